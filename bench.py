@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark: edges/sec into the streaming connected-components summary on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch of synthetic input: reset the summary to its initial
+value, fold this rank's edge chunk (already resident in HBM) window by window into the device forest,
+and emit the summary after every window (canonicalising compress; with N>1 the butterfly forest merge
+over RCCL/xGMI first). Weak scaling: every rank folds the same number of edges of one shared stream
+(rank r owns chunk r), so value = N * edges_per_rank * K / max-over-ranks time.
+
+N=1 default workload: configs[1] = R-MAT scale 20 (1M vertices, 16M edges), one merge window per step.
+Launch: python bench.py [--gpus N --steps K --warmup W]  (N>1 under torch.distributed.run, one rank per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gelly-streaming_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
+BYTES_PER_EDGE = 16  # algorithmic: 8 B edge stream + 2 x 4 B parent reads
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2_rmat20")
+    ap.add_argument("--window-edges", type=int, default=0, help="edges per merge window per rank (0 = config default)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = min(16, cores))")
+    ap.add_argument("--no-parity", action="store_true")
+    return ap.parse_args()
+
+
+def rank_stream(cfg, world):
+    """The shared stream all ranks draw from, and the per-rank edge count (weak scaling)."""
+    from gelly_stream import generators as G
+
+    E1, V = cfg.info()
+    if world > 1 and cfg.kind in (2, 3):  # RMAT / GNM: a world-times longer stream over the same ids
+        cfg = G.scaled(cfg, n_edges=cfg.n_edges * world)
+    return cfg, E1, V
+
+
+def traffic_from_profiles(workload, n_edges):
+    """HBM bytes per fold launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json), or None."""
+    pdir = os.path.join(ROOT, "profiles")
+    best = None
+    if os.path.isdir(pdir):
+        for f in sorted(os.listdir(pdir)):
+            if f.endswith(".json") and "pmc" in f and workload in f:
+                try:
+                    d = json.load(open(os.path.join(pdir, f)))
+                except Exception:
+                    continue
+                if d.get("n_edges") == n_edges and d.get("hbm_bytes_per_launch"):
+                    best = d
+    return best
+
+
+def cpu_baseline(cfg, E, V, target_s, threads):
+    """The CPU oracle (restated reference topology) timed on this host: the same stream, one window."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc  # cpu_baseline leg only
+
+    from gelly_stream import generators as G
+
+    pairs = G.generate_host(cfg, 0, E)
+    starts = [0, E]
+    reps, total, digest = 0, 0.0, None
+    while True:
+        out = orc.cc_stream(pairs, starts, V, partitions=threads, threads=threads, want_digest=(reps == 0))
+        if reps == 0:
+            digest = int(out["digest"][0])
+        total += out["fold_seconds"]
+        reps += 1
+        if total >= target_s or reps >= 50:
+            break
+    return {
+        "value": E * reps / total,
+        "unit": "edges/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"full {cfg.name} stream ({E} edges, 1 window) x {reps} reps = {total:.1f} s; "
+                  f"{threads} partitions/threads folding HashMap union-by-rank DisjointSets + serial CombineCC merge "
+                  f"(oracle/cc_oracle.c); host cores visible: {os.cpu_count()}",
+    }, digest
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    from gelly_stream import generators as G
+    from gelly_stream.distributed import ForestGroup, TorchDisjointSet
+
+    base = G.CONFIGS[args.workload]
+    cfg, E1, V = rank_stream(base, world)
+    W = args.window_edges or base.window_edges or E1
+    starts = list(range(0, E1, W)) + [E1]
+    n_windows = len(starts) - 1
+
+    # edges of this rank's chunk, generated straight into HBM (outside any timed region)
+    d_edges = torch.empty(2 * E1, dtype=torch.int32, device=f"cuda:{local}")
+    stream = torch.cuda.current_stream(local)
+    G.generate_device(cfg, rank * E1, E1, d_edges.data_ptr(), stream.cuda_stream)
+    forest = TorchDisjointSet(V, local)
+    group = ForestGroup() if world > 1 else None
+    base_ptr = d_edges.data_ptr()
+
+    fold_events = []
+
+    def step(timed):
+        forest.ds.reset()
+        for w in range(n_windows):
+            b, e = starts[w], starts[w + 1]
+            if timed:
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record(stream)
+            forest.ds.fold_device(base_ptr + 8 * b, e - b)
+            if timed:
+                ev1.record(stream)
+                fold_events.append((ev0, ev1, e - b))
+            if group is not None:
+                group.merge_forest(forest)
+            else:
+                forest.compress()
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    fold_ms = [a.elapsed_time(b) for a, b, _ in fold_events]
+    fold_edges = [n for _, _, n in fold_events]
+    avg_fold_s = sum(fold_ms) / len(fold_ms) / 1e3
+    avg_launch_edges = sum(fold_edges) / len(fold_edges)
+    achieved = BYTES_PER_EDGE * avg_launch_edges / avg_fold_s / 1e9
+
+    labels = forest.ds.labels()
+    seen = int(np.count_nonzero(labels != 0xFFFFFFFF))
+    comps = int(np.count_nonzero(labels == np.arange(V, dtype=np.uint32)))
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    total_edges = world * E1 * args.steps
+    prof = traffic_from_profiles(args.workload, int(avg_launch_edges))
+    result = {
+        "metric": "edges/sec into CC summary",
+        "value": total_edges / elapsed,
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{base.name}: " + {
+                "c2_rmat20": "R-MAT scale 20 (A,B,C,D=0.57,0.19,0.19,0.05), edge factor 16, seeded permutation",
+                "c3_gnm24": "uniform G(n,m) n=2^24 m=9227469",
+                "c4_kron26": "Kronecker scale 26, edge factor 16",
+                "c5_adversarial": "shuffled 2^23-path + 1024 stars of 8192",
+            }.get(base.name, base.name),
+            "edges_per_gpu": E1,
+            "vertices": V,
+            "windows_per_step": n_windows,
+            "window_edges": W,
+            "parallelism": f"dp{world}",
+            "merge": "butterfly p2p over RCCL" if world > 1 else "none",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "fold_kernel",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": prof["hbm_bytes_per_launch"] if prof else None,
+            "traffic_source": prof["source"] if prof else None,
+            "fold_ms_avg": avg_fold_s * 1e3,
+            "edges_per_launch": int(avg_launch_edges),
+            "bytes_per_edge": BYTES_PER_EDGE,
+        },
+        "summary": {"seen": seen, "components": comps},
+    }
+    if world == 1 and args.cpu_seconds > 0:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cb, digest = cpu_baseline(cfg, E1, V, args.cpu_seconds, threads)
+        result["cpu_baseline"] = cb
+        if not args.no_parity:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as orc
+
+            result["parity"] = "bit-exact" if orc.label_digest(labels) == digest else "MISMATCH"
+    print(json.dumps(result))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

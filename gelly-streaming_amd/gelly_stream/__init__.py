@@ -1,0 +1,21 @@
+"""gelly_stream — MI355X-native streaming connected components (gelly-streaming's CC hot path).
+
+Public surface mirrors the reference's operator API (`…/` = src/main/java/org/apache/flink/graph/streaming/):
+  DisjointSet              …/summaries/DisjointSet.java       (device-resident union-find forest)
+  ConnectedComponents      …/library/ConnectedComponents.java (UpdateCC fold + CombineCC combine)
+  SummaryBulkAggregation   …/SummaryBulkAggregation.java      (window fold -> combine -> Merger)
+  EdgesFold                …/EdgesFold.java
+  SimpleEdgeStream         …/SimpleEdgeStream.java            (constructor + aggregate())
+All device work goes through libgelly_cc.so (include/gelly_cc.h); there is no CPU fallback.
+"""
+from .aggregation import EdgeBatch, EdgesFold, Merger, ReduceFunction, SummaryAggregation, SummaryBulkAggregation
+from .edgestream import SimpleEdgeStream
+from .library import CombineCC, ConnectedComponents, UpdateCC
+from .native import UNSEEN, GellyCCError, device_count
+from .summaries import DisjointSet
+
+__all__ = [
+    "CombineCC", "ConnectedComponents", "DisjointSet", "EdgeBatch", "EdgesFold", "GellyCCError", "Merger",
+    "ReduceFunction", "SimpleEdgeStream", "SummaryAggregation", "SummaryBulkAggregation", "UNSEEN", "UpdateCC",
+    "device_count",
+]

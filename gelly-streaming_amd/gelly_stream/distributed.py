@@ -1,0 +1,109 @@
+"""Cross-GPU combine of the per-rank CC forests (replaces the reference's all-to-one window gather).
+
+Reference: SummaryBulkAggregation.run (…/SummaryBulkAggregation.java:81-83) gathers every partition's
+partial DisjointSet, Kryo-serialised, to ONE task: ``timeWindowAll(t).reduce(CombineCC)`` then the
+parallelism-1 ``Merger`` (…/SummaryAggregation.java:107-119). SummaryTreeReduce (…/SummaryTreeReduce.java:95-123)
+pairs partitions up in a log2 tree instead.
+
+MI355X form: every rank (one process per GPU) keeps a full-range forest. At a window boundary each rank
+compresses its forest to canonical min-id labels and runs a butterfly over torch.distributed point-to-point
+(RCCL over xGMI; gloo in the CPU tests): in round r it swaps its label array with rank ^ 2^r and unions the
+partner's (v, label[v]) pairs into its own forest. After log2(P) rounds every rank holds the global partition
+— exactly the forest the reference's reduce + Merger emit — and no rank is a serial bottleneck. Each round
+moves V * 4 bytes over one direct xGMI link. A non-power-of-two world falls back to all_gather + union.
+"""
+from __future__ import annotations
+
+from typing import Optional, Protocol
+
+
+class ExchangeForest(Protocol):
+    """What the butterfly needs from a forest."""
+
+    def compress(self) -> None: ...                     # canonicalise (async on the comm stream)
+    def exchange_tensor(self): ...                      # torch tensor holding the labels (same device as comms)
+    def absorb(self, labels) -> None: ...               # forest := forest ∪ {(v, labels[v])}
+
+
+class TorchDisjointSet:
+    """A DisjointSet whose parent array is a torch tensor on this rank's GPU and whose HIP stream is torch's
+    current stream, so RCCL collectives issued by torch.distributed order correctly with the HIP kernels."""
+
+    def __init__(self, id_capacity: int, device: int = 0):
+        import torch
+
+        from .summaries import DisjointSet
+
+        self.id_capacity = int(id_capacity)
+        self.device = int(device)
+        self.parent = torch.empty(self.id_capacity, dtype=torch.int32, device=f"cuda:{self.device}")
+        self.ds = DisjointSet(self.id_capacity, self.device, d_parent=self.parent.data_ptr())
+        self.ds.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+        self._recv = None
+
+    # ExchangeForest
+    def compress(self) -> None:
+        self.ds.compress()
+
+    def exchange_tensor(self):
+        return self.parent
+
+    def absorb(self, labels) -> None:
+        self.ds.merge_labels_device(labels.data_ptr(), labels.numel())
+
+    def __getattr__(self, name):  # delegate the DisjointSet surface (find, getMatches, fold_device, ...)
+        return getattr(self.ds, name)
+
+
+class ForestGroup:
+    """Butterfly min-label merge of one forest per rank."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self._dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self._recv = None
+        self._gather = None
+
+    def _global(self, r: int) -> int:
+        return r if self.group is None else self._dist.get_global_rank(self.group, r)
+
+    def _recv_like(self, t):
+        if self._recv is None or self._recv.shape != t.shape or self._recv.device != t.device:
+            self._recv = t.new_empty(t.shape)
+        return self._recv
+
+    def merge_forest(self, forest: ExchangeForest) -> None:
+        """forest := union of every rank's forest (collective: every rank must call it)."""
+        dist = self._dist
+        forest.compress()
+        if self.world == 1:
+            return
+        buf = forest.exchange_tensor()
+        if self.world & (self.world - 1) == 0:
+            recv = self._recv_like(buf)
+            step = 1
+            while step < self.world:
+                partner = self._global(self.rank ^ step)
+                ops = [dist.P2POp(dist.isend, buf, partner, self.group), dist.P2POp(dist.irecv, recv, partner, self.group)]
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+                forest.absorb(recv)
+                forest.compress()
+                step <<= 1
+        else:
+            if self._gather is None or self._gather[0].shape != buf.shape:
+                self._gather = [buf.new_empty(buf.shape) for _ in range(self.world)]
+            dist.all_gather(self._gather, buf, group=self.group)
+            for p, t in enumerate(self._gather):
+                if p != self.rank:
+                    forest.absorb(t)
+            forest.compress()
+
+    def reduce(self, summary, combineFun=None):
+        """SummaryBulkAggregation's timeWindowAll(...).reduce(combineFun) across ranks, for a forest summary."""
+        self.merge_forest(summary)
+        return summary

@@ -1,0 +1,120 @@
+"""ctypes binding of the C ABI declared in include/gelly_cc.h (libgelly_cc.so, built for gfx950).
+
+The product path has no CPU fallback: if the library is missing or no gfx950 device is visible, calls
+raise GellyCCError. Build with ``python -c "import __graft_entry__ as g; g.build()"`` (or ``make -C
+gelly-streaming_amd``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, byref, c_char_p, c_float, c_int, c_uint32, c_uint64, c_void_p
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libgelly_cc.so")
+
+UNSEEN = 0xFFFFFFFF
+
+GCC_GEN_EXAMPLE = 1
+GCC_GEN_RMAT = 2
+GCC_GEN_GNM = 3
+GCC_GEN_ADVERSARIAL = 4
+
+ERRORS = {-1: "GCC_E_INVALID", -2: "GCC_E_HIP", -3: "GCC_E_NODEV", -4: "GCC_E_OOM"}
+
+
+class GellyCCError(RuntimeError):
+    """A C-ABI call returned a negative status (the JNI glue maps the same codes to Java exceptions)."""
+
+    def __init__(self, code: int, fn: str, msg: str):
+        super().__init__(f"{fn}: {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class GenParams(ctypes.Structure):
+    """gcc_gen_params (include/gelly_cc.h)."""
+
+    _fields_ = [
+        ("kind", c_uint32),
+        ("scale", c_uint32),
+        ("n_vertices", c_uint64),
+        ("n_edges", c_uint64),
+        ("seed", c_uint64),
+        ("n_stars", c_uint32),
+        ("star_size", c_uint32),
+        ("permute", c_uint32),
+        ("reserved", c_uint32),
+    ]
+
+
+# exported symbol -> (restype, argtypes); the not-gpu tests check that every symbol in include/*.h is here
+_SIGS = {
+    "gcc_last_error": (c_char_p, []),
+    "gcc_version": (c_int, []),
+    "gcc_device_count": (c_int, [POINTER(c_int)]),
+    "gcc_init": (c_int, [c_int]),
+    "gcc_gen_info": (c_int, [POINTER(GenParams), POINTER(c_uint64), POINTER(c_uint64)]),
+    "gcc_gen_host": (c_int, [POINTER(GenParams), c_uint64, c_uint64, c_void_p]),
+    "gcc_gen_device": (c_int, [POINTER(GenParams), c_uint64, c_uint64, c_void_p, c_void_p]),
+    "gcc_forest_create": (c_int, [c_int, c_uint32, POINTER(c_void_p)]),
+    "gcc_forest_create_ext": (c_int, [c_int, c_uint32, c_void_p, POINTER(c_void_p)]),
+    "gcc_forest_destroy": (c_int, [c_void_p]),
+    "gcc_forest_set_stream": (c_int, [c_void_p, c_void_p]),
+    "gcc_forest_get_stream": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "gcc_forest_capacity": (c_int, [c_void_p, POINTER(c_uint32)]),
+    "gcc_forest_device_ptr": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "gcc_forest_reset": (c_int, [c_void_p]),
+    "gcc_forest_union": (c_int, [c_void_p, c_uint32, c_uint32]),
+    "gcc_forest_make_set": (c_int, [c_void_p, c_uint32]),
+    "gcc_forest_staging": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64)]),
+    "gcc_forest_submit": (c_int, [c_void_p, c_uint64]),
+    "gcc_forest_fold_host": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_forest_fold_device": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_forest_flush": (c_int, [c_void_p]),
+    "gcc_forest_sync": (c_int, [c_void_p]),
+    "gcc_forest_merge": (c_int, [c_void_p, c_void_p]),
+    "gcc_forest_merge_labels_device": (c_int, [c_void_p, c_void_p, c_uint32]),
+    "gcc_forest_compress": (c_int, [c_void_p]),
+    "gcc_forest_labels": (c_int, [c_void_p, c_void_p, c_uint32]),
+    "gcc_forest_find": (c_int, [c_void_p, c_uint32, POINTER(c_uint32)]),
+    "gcc_forest_size": (c_int, [c_void_p, POINTER(c_uint64)]),
+    "gcc_forest_count_components": (c_int, [c_void_p, POINTER(c_uint64)]),
+    "gcc_forest_import_pairs": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_forest_enable_timing": (c_int, [c_void_p, c_int]),
+    "gcc_forest_last_fold_ms": (c_int, [c_void_p, POINTER(c_float)]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libgelly_cc.so (once). Raises GellyCCError if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise GellyCCError(-3, "load", f"{LIB_PATH} not found: build it first (__graft_entry__.build())")
+        l = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    """Call a status-returning C-ABI function; raise GellyCCError on a negative status."""
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().gcc_last_error()
+        raise GellyCCError(rc, name, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    n = c_int(0)
+    call("gcc_device_count", byref(n))
+    return n.value
+
+
+def exported_symbols() -> list[str]:
+    return sorted(_SIGS)

@@ -1,0 +1,127 @@
+/*
+ * gelly_cc.h — C ABI of the MI355X-native streaming connected-components summary.
+ *
+ * This is the drop-in boundary for gelly-streaming's one data-parallel hot path:
+ *   SimpleEdgeStream.aggregate(new ConnectedComponents(mergeWindowTime))
+ *   -> SummaryBulkAggregation: fold DisjointSet.union over each edge partition per window,
+ *      combine the partial forests with CombineCC (DisjointSet.merge), running summary in Merger.
+ * Reference files (relative to the reference repo, `…/` = src/main/java/org/apache/flink/graph/streaming/):
+ *   …/summaries/DisjointSet.java        (makeSet :58-61, find :71-85, union :97-123, merge :132-136,
+ *                                         getMatches :49-51, toString :139-153)
+ *   …/library/ConnectedComponents.java  (UpdateCC.foldEdges :83-86, CombineCC.reduce :116-125)
+ *   …/SummaryBulkAggregation.java       (PartialAgg.fold :121-123, timeWindowAll.reduce :81-82)
+ *   …/SummaryAggregation.java           (Merger.flatMap :107-119, snapshotState/restoreState :127-135)
+ * Each entry point below names the reference method it replaces. A JNI / Panama-FFM binding for the
+ * Java side is given in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Vertex ids are u32 in [0, id_capacity); id_capacity <= 0xFFFFFFFF. GCC_UNSEEN (0xFFFFFFFF) marks a
+ *    vertex that is not in the summary's key set (DisjointSet.getMatches().containsKey(v) == false).
+ *  - Canonical labels: label[v] = min{u : u ~ v} over the edges folded so far, GCC_UNSEEN if unseen.
+ *    Partition parity with the reference is defined on these labels (union-by-rank roots are not part
+ *    of the contract; DisjointSet.java:113-122 only changes which root is chosen).
+ *  - Edge batches are interleaved u32 pairs (src0, dst0, src1, dst1, ...), 8 bytes per edge.
+ *  - Every function returns 0 on success or a negative GCC_E* code; gcc_last_error() returns a
+ *    thread-local message for the last failure on the calling thread. No C++ exception crosses the ABI.
+ *  - Threading: one forest handle is used by one thread at a time (a Flink task thread calls fold /
+ *    reduce / flatMap serially on one accumulator); different handles may be used concurrently.
+ *  - Each forest owns (or is given, gcc_forest_set_stream) one hipStream_t; all device work of the
+ *    handle is ordered on it. Reads that return data to the host synchronise that stream first.
+ */
+#ifndef GELLY_CC_H
+#define GELLY_CC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GCC_UNSEEN 0xFFFFFFFFu
+
+/* error codes */
+#define GCC_OK 0
+#define GCC_E_INVALID (-1) /* bad argument (null handle, id out of range, size mismatch) */
+#define GCC_E_HIP (-2)     /* a HIP runtime call failed */
+#define GCC_E_NODEV (-3)   /* no usable gfx950 device */
+#define GCC_E_OOM (-4)     /* device or pinned-host allocation failed */
+
+/* ---- generator parameters (synthetic edge streams; see gelly-streaming_amd/csrc/edge_gen.h) ---- */
+enum {
+    GCC_GEN_EXAMPLE = 1,     /* ConnectedComponentsExample default data (…/example/ConnectedComponentsExample.java:121-133) */
+    GCC_GEN_RMAT = 2,        /* R-MAT / Kronecker (0.57, 0.19, 0.19, 0.05) */
+    GCC_GEN_GNM = 3,         /* uniform G(n, m) */
+    GCC_GEN_ADVERSARIAL = 4, /* shuffled long path + stars */
+};
+
+typedef struct gcc_gen_params {
+    uint32_t kind;       /* GCC_GEN_* */
+    uint32_t scale;      /* RMAT: log2(V); ADVERSARIAL: path bits P */
+    uint64_t n_vertices; /* GNM: n */
+    uint64_t n_edges;    /* RMAT / GNM: number of edges */
+    uint64_t seed;
+    uint32_t n_stars;    /* ADVERSARIAL: number of stars S */
+    uint32_t star_size;  /* ADVERSARIAL: ids per star L (hub + L-1 leaves) */
+    uint32_t permute;    /* RMAT: 1 = seeded vertex permutation */
+    uint32_t reserved;
+} gcc_gen_params;
+
+typedef struct gcc_forest gcc_forest; /* opaque: one device-resident union-find forest (one DisjointSet) */
+
+/* ---- process / device ---- */
+const char* gcc_last_error(void);
+int gcc_version(void); /* ABI version, 1 */
+int gcc_device_count(int* n);
+int gcc_init(int device); /* select + warm up one device (optional; create does it lazily) */
+
+/* ---- generators (no reference counterpart: synthetic inputs for the benchmark configs) ---- */
+int gcc_gen_info(const gcc_gen_params* p, uint64_t* n_edges, uint64_t* n_vertices);
+int gcc_gen_host(const gcc_gen_params* p, uint64_t first, uint64_t count, uint32_t* out_pairs);
+int gcc_gen_device(const gcc_gen_params* p, uint64_t first, uint64_t count, uint32_t* d_out_pairs, void* hip_stream);
+
+/* ---- forest lifetime: `new DisjointSet<>()` (DisjointSet.java:36-39) ---- */
+int gcc_forest_create(int device, uint32_t id_capacity, gcc_forest** out);
+/* same, over caller-owned device memory of id_capacity u32 (e.g. a torch tensor); not freed by destroy */
+int gcc_forest_create_ext(int device, uint32_t id_capacity, uint32_t* d_parent, gcc_forest** out);
+int gcc_forest_destroy(gcc_forest* h);
+int gcc_forest_set_stream(gcc_forest* h, void* hip_stream); /* NULL = the handle's own stream */
+int gcc_forest_get_stream(gcc_forest* h, void** hip_stream);
+int gcc_forest_capacity(gcc_forest* h, uint32_t* id_capacity);
+int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent); /* parent / label array, id_capacity u32 */
+/* back to the initial value (SummaryAggregation.Merger transientState reset, :113-115; fresh fold value) */
+int gcc_forest_reset(gcc_forest* h);
+
+/* ---- fold: UpdateCC.foldEdges -> DisjointSet.union (ConnectedComponents.java:83-86, DisjointSet.java:97-123) ---- */
+int gcc_forest_union(gcc_forest* h, uint32_t u, uint32_t v); /* one edge, appended to pinned staging */
+int gcc_forest_make_set(gcc_forest* h, uint32_t v);          /* DisjointSet.makeSet (:58-61) = union(v, v) */
+int gcc_forest_staging(gcc_forest* h, uint32_t** pairs, uint64_t* cap_edges); /* pinned host staging buffer */
+int gcc_forest_submit(gcc_forest* h, uint64_t n_edges);      /* fold the first n_edges of staging (async) */
+int gcc_forest_fold_host(gcc_forest* h, const uint32_t* pairs, uint64_t n_edges); /* pageable host pairs */
+int gcc_forest_fold_device(gcc_forest* h, const uint32_t* d_pairs, uint64_t n_edges); /* pairs in HBM, async */
+int gcc_forest_flush(gcc_forest* h); /* launch any staged single-edge unions */
+int gcc_forest_sync(gcc_forest* h);  /* flush + wait for the handle's stream */
+
+/* ---- combine: CombineCC.reduce / DisjointSet.merge (ConnectedComponents.java:116-125, DisjointSet.java:132-136) ---- */
+int gcc_forest_merge(gcc_forest* into, gcc_forest* from); /* into := into ∪ from (any two devices) */
+/* into := into ∪ {(v, labels[v]) : labels[v] != GCC_UNSEEN}; d_labels: n u32 in HBM of into's device,
+ * ordered on into's stream (the receive side of the cross-GPU merge) */
+int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, uint32_t n);
+
+/* ---- summary reads (DisjointSet.find :71-85, getMatches :49-51; the emitted summary per window) ---- */
+int gcc_forest_compress(gcc_forest* h); /* async: parent[v] := canonical label; device array becomes labels */
+int gcc_forest_labels(gcc_forest* h, uint32_t* out, uint32_t n); /* compress + copy n labels to host */
+int gcc_forest_find(gcc_forest* h, uint32_t v, uint32_t* root); /* canonical root; GCC_UNSEEN = Java null */
+int gcc_forest_size(gcc_forest* h, uint64_t* n_seen);            /* getMatches().size() */
+int gcc_forest_count_components(gcc_forest* h, uint64_t* n_components);
+/* restore / deserialize: fold (key, parent) pairs (Merger.restoreState :132-135 + Kryo path) */
+int gcc_forest_import_pairs(gcc_forest* h, const uint32_t* pairs, uint64_t n_pairs);
+
+/* ---- measurement: duration of the last fold launch (HIP events on the handle's stream) ---- */
+int gcc_forest_enable_timing(gcc_forest* h, int enable);
+int gcc_forest_last_fold_ms(gcc_forest* h, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GELLY_CC_H */

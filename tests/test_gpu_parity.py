@@ -1,0 +1,326 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle and the golden fixtures. Bit-exact labels.
+
+Canonical form (the parity contract): after every merge window, label[v] = min id of v's
+component over all edges folded so far, 0xFFFFFFFF for ids never seen. Run with: pytest -m gpu
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from gelly_stream import (ConnectedComponents, DisjointSet, GellyCCError, SimpleEdgeStream, native)
+from gelly_stream import generators as G
+
+pytestmark = pytest.mark.gpu
+UNSEEN = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    return torch
+
+
+def device_stream(torch_cuda, cfg, first=0, count=None):
+    """Generate edges straight into HBM (a torch tensor as plain device memory) and return it."""
+    E, _ = cfg.info()
+    count = E - first if count is None else count
+    t = torch_cuda.empty(2 * max(count, 1), dtype=torch_cuda.int32, device="cuda:0")
+    G.generate_device(cfg, first, count, t.data_ptr(), 0)
+    torch_cuda.cuda.synchronize()
+    return t
+
+
+def first_mismatch(got, want):
+    bad = np.flatnonzero(got != want)
+    return None if bad.size == 0 else (int(bad[0]), int(got[bad[0]]), int(want[bad[0]]), int(bad.size))
+
+
+def test_native_library_is_the_in_tree_build():
+    native.lib()
+    maps = open("/proc/self/maps").read()
+    assert native.LIB_PATH in maps
+    assert native.device_count() >= 1
+
+
+# ---- DisjointSetTest replayed on the GPU summary (util/DisjointSetTest.java:36-78) ----
+@pytest.fixture()
+def gpu_ds(golden):
+    fx = golden("kat_disjoint_set.json")
+    ds = DisjointSet(128)
+    for a, b in fx["setup_edges"]:
+        ds.union(a, b)
+    yield ds, fx
+    ds.close()
+
+
+def test_get_matches(gpu_ds):
+    ds, fx = gpu_ds
+    assert ds.getMatches().size() == fx["size"] == 10
+    assert sorted(ds.getMatches().keySet()) == list(range(10))
+
+
+def test_find(gpu_ds):
+    ds, fx = gpu_ds
+    root1, root2 = ds.find(0), ds.find(1)
+    assert root1 != root2
+    for i in range(10):
+        assert ds.find(i) == (root1 if i % 2 == 0 else root2)
+    assert ds.find(50) is None
+    assert {str(k): int(v) for k, v in enumerate(ds.labels()[:10])} == fx["labels"]
+
+
+def test_merge(gpu_ds):
+    ds, fx = gpu_ds
+    ds2 = DisjointSet(128)
+    for a, b in fx["ds2_edges"]:
+        ds2.union(a, b)
+    ds2.merge(ds)
+    assert ds2.getMatches().size() == 18
+    roots = {ds2.find(k) for k in ds2.getMatches().keySet()}
+    assert len(roots) == 2
+    lab = ds2.labels()
+    assert {k: int(lab[int(k)]) for k in fx["merged_labels"]} == fx["merged_labels"]
+    assert ds.getMatches().size() == 10  # merge leaves `other` unchanged
+
+
+def test_to_string(gpu_ds):
+    ds, _ = gpu_ds
+    assert str(ds) == "{0=[0, 2, 4, 6, 8], 1=[1, 3, 5, 7, 9]}"
+
+
+# ---- ConnectedComponentsTest (example/test/ConnectedComponentsTest.java) ----
+def test_connected_components_job(golden):
+    fx = golden("kat_connected_components.json")
+    cc = ConnectedComponents(mergeWindowTime=5, id_capacity=10)
+    outs = [s.labels().copy() for s in SimpleEdgeStream(np.array(fx["edges"])).aggregate(cc)]
+    assert outs[-1].tolist() == fx["labels"]
+    comps = {}
+    for v in np.flatnonzero(outs[-1] != UNSEEN):
+        comps.setdefault(int(outs[-1][v]), []).append(int(v))
+    assert sorted(comps.values()) == fx["components"]
+    assert len(comps) == 3  # :73
+
+
+# ---- ConnectedComponentsExample default data: 11 event-time windows ----
+def test_example_default_windows(golden):
+    fx = golden("example_default.json")
+    cfg = G.CONFIGS["c1_example"]
+    stream = SimpleEdgeStream(G.generate_host(cfg), timestamps=G.timestamps(cfg))
+    cc = ConnectedComponents(mergeWindowTime=cfg.merge_window_ms, id_capacity=fx["V"])
+    got = [s.labels().copy() for s in stream.aggregate(cc)]
+    assert len(got) == 11
+    for w, entry in enumerate(fx["windows"]):
+        assert got[w].tolist() == entry["labels"], w
+
+
+# ---- small synthetic streams vs fixtures: host-fed and device-resident paths ----
+STREAMS = {
+    "stream_rmat_s10.json": lambda g: G.scaled(G.CONFIGS["c2_rmat20"], scale=g["scale"], n_edges=g["n_edges"], seed=g["seed"]),
+    "stream_gnm_4096.json": lambda g: G.scaled(G.CONFIGS["c3_gnm24"], n_vertices=g["n_vertices"], n_edges=g["n_edges"], seed=g["seed"]),
+    "stream_adversarial_p10.json": lambda g: G.scaled(G.CONFIGS["c5_adversarial"], scale=g["scale"], n_stars=g["n_stars"],
+                                                       star_size=g["star_size"], seed=g["seed"]),
+}
+
+
+def check_windows(summaries_iter, fx):
+    n = 0
+    for w, s in enumerate(summaries_iter):
+        lab = s.labels()
+        entry = fx["windows"][w]
+        assert str(orc.label_digest(lab)) == entry["digest"], (fx["name"], w)
+        assert s.getMatches().size() == entry["seen"]
+        assert s.num_components() == entry["components"]
+        if "labels" in entry:
+            assert lab.tolist() == entry["labels"]
+        n += 1
+    assert n == len(fx["windows"])
+
+
+@pytest.mark.parametrize("name", sorted(STREAMS))
+def test_stream_fixture_host_fed(golden, name):
+    fx = golden(name)
+    cfg = STREAMS[name](fx["generator"])
+    pairs = G.generate_host(cfg)
+    starts = np.asarray(fx["window_starts"])
+    stream = SimpleEdgeStream(pairs, edges_per_window=int(starts[1] - starts[0]))
+    check_windows(stream.aggregate(ConnectedComponents(1000, id_capacity=fx["V"])), fx)
+
+
+@pytest.mark.parametrize("name", sorted(STREAMS))
+def test_stream_fixture_device_resident(golden, torch_cuda, name):
+    fx = golden(name)
+    cfg = STREAMS[name](fx["generator"])
+    d = device_stream(torch_cuda, cfg)
+    host = d.cpu().numpy().view(np.uint32).reshape(-1, 2)
+    assert hashlib.sha256(host.astype("<u4").tobytes()).hexdigest() == fx["edges_sha256"]  # device generator
+    stream = SimpleEdgeStream(device_ptr=d.data_ptr(), n_device_edges=fx["n_edges"],
+                              device_window_starts=np.asarray(fx["window_starts"]))
+    check_windows(stream.aggregate(ConnectedComponents(1000, id_capacity=fx["V"])), fx)
+
+
+# ---- full-size configs vs the oracle, per window ----
+def run_device_windows(torch_cuda, cfg, starts, V):
+    d = device_stream(torch_cuda, cfg)
+    ds = DisjointSet(V)
+    out = []
+    for w in range(len(starts) - 1):
+        b, e = int(starts[w]), int(starts[w + 1])
+        ds.fold_device(d.data_ptr() + 8 * b, e - b)
+        out.append(ds.labels().copy())
+    ds.close()
+    return out
+
+
+@pytest.mark.parametrize("cfg_name,window", [("c2_rmat20", 1 << 20), ("c2_rmat20", 1 << 24), ("c3_gnm24", 1 << 22)])
+def test_full_config_parity(torch_cuda, cfg_name, window):
+    cfg = G.CONFIGS[cfg_name]
+    E, V = cfg.info()
+    starts = np.asarray(list(range(0, E, window)) + [E], dtype=np.uint64)
+    pairs = G.generate_host(cfg)
+    want = orc.cc_stream(pairs, starts, V, partitions=4, threads=4)
+    got = run_device_windows(torch_cuda, cfg, starts, V)
+    for w, lab in enumerate(got):
+        assert orc.label_digest(lab) == int(want["digest"][w]), (cfg_name, w)
+        seen = lab != UNSEEN
+        assert int(seen.sum()) == int(want["seen"][w])
+        assert int(np.count_nonzero(lab[seen] == np.flatnonzero(seen))) == int(want["components"][w])
+
+
+def test_adversarial_prefix_windows(torch_cuda):
+    """C5's short windows (2^16 edges) over the first 2^20 edges, every window vs the oracle."""
+    cfg = G.CONFIGS["c5_adversarial"]
+    _, V = cfg.info()
+    n = 1 << 20
+    starts = np.arange(0, n + 1, cfg.window_edges, dtype=np.uint64)
+    pairs = G.generate_host(cfg, 0, n)
+    want = orc.cc_stream(pairs, starts, V, partitions=2, threads=2)
+    got = run_device_windows(torch_cuda, cfg, starts, V)
+    for w, lab in enumerate(got):
+        assert orc.label_digest(lab) == int(want["digest"][w]), w
+
+
+def test_adversarial_full_stream_closed_form(torch_cuda):
+    """Full C5 (16.7M edges, 256 windows): the final partition is known in closed form — the whole path is one
+    component labelled 0, each star is one component labelled by its hub (its smallest id)."""
+    cfg = G.CONFIGS["c5_adversarial"]
+    E, V = cfg.info()
+    d = device_stream(torch_cuda, cfg)
+    ds = DisjointSet(V)
+    for b in range(0, E, cfg.window_edges):
+        ds.fold_device(d.data_ptr() + 8 * b, min(cfg.window_edges, E - b))
+        ds.compress()
+    lab = ds.labels()
+    P = 1 << cfg.scale
+    assert np.all(lab[:P] == 0)
+    ids = np.arange(P, V, dtype=np.int64)
+    assert np.array_equal(lab[P:], (P + (ids - P) // cfg.star_size * cfg.star_size).astype(np.uint32))
+    assert ds.num_components() == 1 + cfg.n_stars
+
+
+# ---- size-independent properties at full size ----
+def test_order_invariance_and_idempotence(torch_cuda):
+    cfg = G.CONFIGS["c2_rmat20"]
+    E, V = cfg.info()
+    d = device_stream(torch_cuda, cfg)
+    a = DisjointSet(V)
+    a.fold_device(d.data_ptr(), E)
+    la = a.labels().copy()
+    # fold the same stream again: unchanged (idempotence)
+    a.fold_device(d.data_ptr(), E)
+    assert np.array_equal(a.labels(), la)
+    # a permuted stream gives the same partition (order invariance)
+    perm = torch_cuda.randperm(E, device="cuda:0", generator=torch_cuda.Generator(device="cuda:0").manual_seed(7))
+    shuffled = d.view(-1, 2)[perm].contiguous()
+    b = DisjointSet(V)
+    b.fold_device(shuffled.data_ptr(), E)
+    assert np.array_equal(b.labels(), la)
+    # split into two partitions folded separately, then CombineCC-merged: same partition
+    c1, c2 = DisjointSet(V), DisjointSet(V)
+    c1.fold_device(d.data_ptr(), E // 3)
+    c2.fold_device(d.data_ptr() + 8 * (E // 3), E - E // 3)
+    c2.merge(c1)
+    assert np.array_equal(c2.labels(), la)
+    # merging into an empty forest copies the partition; reset empties it
+    e = DisjointSet(V)
+    e.merge(a)
+    assert np.array_equal(e.labels(), la)
+    e.reset()
+    assert e.size() == 0 and np.all(e.labels() == UNSEEN)
+    for x in (a, b, c1, c2, e):
+        x.close()
+
+
+def test_edge_cases():
+    ds = DisjointSet(1 << 10)
+    ds.fold(np.zeros((0, 2), dtype=np.uint32))  # empty batch
+    assert ds.size() == 0 and ds.num_components() == 0
+    ds.union(5, 5)  # self loop = makeSet
+    assert ds.find(5) == 5 and ds.size() == 1
+    ds.fold(np.array([[1023, 1022], [1023, 1022], [1022, 1023]], dtype=np.uint32))  # max id, duplicates
+    assert ds.find(1023) == 1022 and ds.size() == 3
+    ds.makeSet(7)
+    assert ds.find(7) == 7
+    with pytest.raises(GellyCCError):
+        ds.fold(np.array([[1, 1024]], dtype=np.uint32))  # out of range: rejected on the host, no device access
+    with pytest.raises(ValueError):
+        ds.union(0, 4096)
+    one = DisjointSet(1)
+    one.union(0, 0)
+    assert one.labels().tolist() == [0]
+
+
+def test_single_edge_staging_path_crosses_batches():
+    """Per-edge foldEdges calls (the Java drop-in pattern) staged in pinned memory across several batches."""
+    V = 1 << 12
+    rng = np.random.default_rng(3)
+    pairs = rng.integers(0, V, size=(1 << 21) + 17, dtype=np.uint32).reshape(-1, 2)  # > one staging slot
+    ds = DisjointSet(V)
+    for u, v in pairs[:5000]:
+        ds.union(int(u), int(v))
+    ds.fold(pairs[5000:])
+    want = orc.cc_stream(pairs, [0, len(pairs)], V, want_labels=True)["labels"][0]
+    assert first_mismatch(ds.labels(), want) is None
+
+
+def test_snapshot_restore_round_trip():
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=14, n_edges=1 << 17)
+    E, V = cfg.info()
+    ds = DisjointSet(V)
+    ds.fold(G.generate_host(cfg))
+    snap = ds.snapshot_pairs()  # Merger.snapshotState
+    re = DisjointSet(V)
+    re.import_pairs(snap)       # Merger.restoreState
+    assert np.array_equal(re.labels(), ds.labels())
+
+
+def test_hub_contention_star():
+    """Every edge hits one hub (worst-case CAS contention on one parent slot)."""
+    V = 1 << 20
+    leaves = np.arange(1, V, dtype=np.uint32)
+    pairs = np.stack([np.zeros_like(leaves), leaves], axis=1)
+    pairs[::2] = pairs[::2, ::-1]
+    ds = DisjointSet(V)
+    ds.fold(pairs)
+    assert np.all(ds.labels() == 0)
+
+
+def test_descending_path_worst_case_chain():
+    """A path fed from the high end hooks one root under the next smaller one: longest possible chains."""
+    V = 1 << 20
+    hi = np.arange(V - 1, 0, -1, dtype=np.uint32)
+    ds = DisjointSet(V)
+    ds.fold(np.stack([hi, hi - 1], axis=1))
+    assert np.all(ds.labels() == 0)
+
+
+def test_fold_timing_events():
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=16, n_edges=1 << 20)
+    E, V = cfg.info()
+    ds = DisjointSet(V)
+    ds.enable_timing(True)
+    ds.fold(G.generate_host(cfg))
+    assert ds.last_fold_ms() > 0.0
