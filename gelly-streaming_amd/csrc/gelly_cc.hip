@@ -86,7 +86,9 @@ __device__ __forceinline__ u32 seen_parent(u32* parent, u32 v) {
 // find (DisjointSet.find :71-85) from x whose observed parent is p, with path splitting: every visited
 // non-root slot is re-pointed at its grandparent (plain store; see the memory-model note at the top).
 __device__ __forceinline__ u32 find_from(u32* parent, u32 x, u32 p) {
-    if (p == x) return x;
+    // p >= x: x is a root, or p is a stale UNSEEN (an L1 line older than x's makeSet CAS): treat x as a root —
+    // a later CAS on it compares against the real value
+    if (p >= x) return x;
     u32 prev = x, cur = p;
     while (true) {
         const u32 next = parent[cur];
@@ -150,18 +152,19 @@ __global__ __launch_bounds__(kBlock) void merge_labels_kernel(u32* __restrict__ 
     }
 }
 
-// Full compression: parent[v] := root(v) = min id of v's component (multi-level pointer jumping). Runs
-// after a kernel boundary, so no hook is in flight; concurrent writes only shorten chains.
-__global__ __launch_bounds__(kBlock) void compress_kernel(u32* __restrict__ parent, u32 n) {
+// Canonicalise: labels[v] := root(v) = min id of v's component, UNSEEN stays UNSEEN (multi-level pointer
+// jumping). Out of place on purpose: the path-splitting stores that let all threads collapse a deep chain
+// together (O(log d) instead of O(d) per thread) write intermediate ancestors into parent[], and such a store
+// can land after another thread's final root store — in place that would leave a vertex pointing at a
+// non-root. labels[] is written exactly once per slot, by its own thread, so it is race-free; parent[] only
+// needs to stay a valid forest (every store is an ancestor, roots never move: no hook is in flight).
+// Algorithmic traffic: 4 B read + 4 B write per id (chain reads hit L2).
+__global__ __launch_bounds__(kBlock) void compress_kernel(u32* __restrict__ parent, u32* __restrict__ labels, u32 n) {
     const u64 stride = (u64)gridDim.x * kBlock;
     for (u64 vv = (u64)blockIdx.x * kBlock + threadIdx.x; vv < n; vv += stride) {
         const u32 v = (u32)vv;
         const u32 p = parent[v];
-        if (p >= v) continue;  // root or UNSEEN
-        // path splitting on the way up: all threads shorten shared chains together, so a chain of depth d
-        // collapses in O(log d) rounds instead of every thread walking it alone (O(d^2) on a long path)
-        const u32 r = find_from(parent, v, p);
-        if (r != p) parent[v] = r;
+        labels[v] = (p >= v) ? p : find_from(parent, v, p);  // root / UNSEEN: itself
     }
 }
 
@@ -222,8 +225,12 @@ constexpr unsigned kMaxGrid = 2048;
 struct gcc_forest {
     int device = 0;
     u32 cap = 0;
+    // two id-range buffers: d_parent (the working forest) and d_spare; compress writes the canonical labels
+    // into d_spare and the two swap roles, so after a compress d_parent IS the label array
     u32* d_parent = nullptr;
-    bool own_parent = true;
+    u32* d_spare = nullptr;
+    bool own_bufs = true;
+    bool compressed = false;  // d_parent holds canonical labels (no mutation since the last compress)
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
 
@@ -284,6 +291,7 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
         h->t_recorded = true;
     }
     h->host_valid = false;
+    h->compressed = false;
     return GCC_OK;
 }
 
@@ -321,9 +329,12 @@ static int flush(gcc_forest* h) {
 static int compress_async(gcc_forest* h) {
     int rc = flush(h);
     if (rc) return rc;
+    if (h->compressed) return GCC_OK;
     hipLaunchKernelGGL(compress_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent,
-                       h->cap);
+                       h->d_spare, h->cap);
     HIP_TRY(hipGetLastError());
+    std::swap(h->d_parent, h->d_spare);
+    h->compressed = true;
     return GCC_OK;
 }
 
@@ -411,7 +422,8 @@ int gcc_gen_device(const gcc_gen_params* p, uint64_t first, uint64_t count, uint
     return GCC_OK;
 }
 
-static int forest_create_impl(int device, uint32_t id_capacity, uint32_t* d_parent, gcc_forest** out) {
+static int forest_create_impl(int device, uint32_t id_capacity, uint32_t* d_buf0, uint32_t* d_buf1,
+                              gcc_forest** out) {
     CHECK_ARG(out, "out is null");
     *out = nullptr;
     CHECK_ARG(id_capacity >= 1 && id_capacity <= UNSEEN, "id_capacity must be in [1, 0xFFFFFFFF]");
@@ -428,12 +440,14 @@ static int forest_create_impl(int device, uint32_t id_capacity, uint32_t* d_pare
     hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) return fail(set_err(GCC_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e)));
     h->stream = h->own_stream;
-    if (d_parent) {
-        h->d_parent = d_parent;
-        h->own_parent = false;
+    if (d_buf0) {
+        h->d_parent = d_buf0;
+        h->d_spare = d_buf1;
+        h->own_bufs = false;
     } else {
         e = hipMalloc((void**)&h->d_parent, (size_t)id_capacity * sizeof(u32));
-        if (e != hipSuccess) return fail(set_err(GCC_E_OOM, "hipMalloc parent[%u]: %s", id_capacity, hipGetErrorString(e)));
+        if (e == hipSuccess) e = hipMalloc((void**)&h->d_spare, (size_t)id_capacity * sizeof(u32));
+        if (e != hipSuccess) return fail(set_err(GCC_E_OOM, "hipMalloc 2 x u32[%u]: %s", id_capacity, hipGetErrorString(e)));
     }
     e = hipEventCreate(&h->t0);
     if (e == hipSuccess) e = hipEventCreate(&h->t1);
@@ -445,12 +459,12 @@ static int forest_create_impl(int device, uint32_t id_capacity, uint32_t* d_pare
 }
 
 int gcc_forest_create(int device, uint32_t id_capacity, gcc_forest** out) {
-    return forest_create_impl(device, id_capacity, nullptr, out);
+    return forest_create_impl(device, id_capacity, nullptr, nullptr, out);
 }
 
-int gcc_forest_create_ext(int device, uint32_t id_capacity, uint32_t* d_parent, gcc_forest** out) {
-    CHECK_ARG(d_parent, "d_parent is null");
-    return forest_create_impl(device, id_capacity, d_parent, out);
+int gcc_forest_create_ext(int device, uint32_t id_capacity, uint32_t* d_buf0, uint32_t* d_buf1, gcc_forest** out) {
+    CHECK_ARG(d_buf0 && d_buf1 && d_buf0 != d_buf1, "need two distinct device buffers");
+    return forest_create_impl(device, id_capacity, d_buf0, d_buf1, out);
 }
 
 int gcc_forest_destroy(gcc_forest* h) {
@@ -462,7 +476,10 @@ int gcc_forest_destroy(gcc_forest* h) {
         if (h->d_stage[s]) (void)hipFree(h->d_stage[s]);
         if (h->stage_ev[s]) (void)hipEventDestroy(h->stage_ev[s]);
     }
-    if (h->own_parent && h->d_parent) (void)hipFree(h->d_parent);
+    if (h->own_bufs) {
+        if (h->d_parent) (void)hipFree(h->d_parent);
+        if (h->d_spare) (void)hipFree(h->d_spare);
+    }
     if (h->d_scratch) (void)hipFree(h->d_scratch);
     if (h->d_counts) (void)hipFree(h->d_counts);
     if (h->t0) (void)hipEventDestroy(h->t0);
@@ -514,6 +531,7 @@ int gcc_forest_reset(gcc_forest* h) {
     h->staged = 0;
     HIP_TRY(hipMemsetAsync(h->d_parent, 0xFF, (size_t)h->cap * sizeof(u32), h->stream));
     h->host_valid = false;
+    h->compressed = true;  // all UNSEEN is canonical
     return GCC_OK;
 }
 
@@ -622,6 +640,7 @@ int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, u
                        d_labels, n);
     HIP_TRY(hipGetLastError());
     into->host_valid = false;
+    into->compressed = false;
     return GCC_OK;
 }
 
@@ -677,6 +696,18 @@ int gcc_forest_labels(gcc_forest* h, uint32_t* out, uint32_t n) {
     int rc = refresh_host(h);
     if (rc) return rc;
     std::memcpy(out, h->host_labels.data(), (size_t)n * sizeof(u32));
+    return GCC_OK;
+}
+
+int gcc_forest_raw_parent(gcc_forest* h, uint32_t* out, uint32_t n) {
+    CHECK_ARG(h, "null forest");
+    CHECK_ARG(out || n == 0, "out is null");
+    CHECK_ARG(n <= h->cap, "n exceeds id_capacity");
+    DeviceGuard g(h->device);
+    int rc = flush(h);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out, h->d_parent, (size_t)n * sizeof(u32), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
     return GCC_OK;
 }
 

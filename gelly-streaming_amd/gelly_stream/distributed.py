@@ -26,8 +26,8 @@ class ExchangeForest(Protocol):
 
 
 class TorchDisjointSet:
-    """A DisjointSet whose parent array is a torch tensor on this rank's GPU and whose HIP stream is torch's
-    current stream, so RCCL collectives issued by torch.distributed order correctly with the HIP kernels."""
+    """A DisjointSet whose two id-range buffers are torch tensors on this rank's GPU and whose HIP stream is
+    torch's current stream, so RCCL collectives issued by torch.distributed order correctly with the kernels."""
 
     def __init__(self, id_capacity: int, device: int = 0):
         import torch
@@ -36,17 +36,18 @@ class TorchDisjointSet:
 
         self.id_capacity = int(id_capacity)
         self.device = int(device)
-        self.parent = torch.empty(self.id_capacity, dtype=torch.int32, device=f"cuda:{self.device}")
-        self.ds = DisjointSet(self.id_capacity, self.device, d_parent=self.parent.data_ptr())
+        self.bufs = [torch.empty(self.id_capacity, dtype=torch.int32, device=f"cuda:{self.device}") for _ in range(2)]
+        self.ds = DisjointSet(self.id_capacity, self.device, d_buffers=(self.bufs[0].data_ptr(), self.bufs[1].data_ptr()))
         self.ds.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
-        self._recv = None
 
     # ExchangeForest
     def compress(self) -> None:
         self.ds.compress()
 
     def exchange_tensor(self):
-        return self.parent
+        """The tensor that currently holds the forest (the canonical labels right after compress())."""
+        cur = self.ds.device_ptr()
+        return self.bufs[0] if self.bufs[0].data_ptr() == cur else self.bufs[1]
 
     def absorb(self, labels) -> None:
         self.ds.merge_labels_device(labels.data_ptr(), labels.numel())
@@ -87,6 +88,7 @@ class ForestGroup:
             recv = self._recv_like(buf)
             step = 1
             while step < self.world:
+                buf = forest.exchange_tensor()  # compress swaps buffers: fetch the current labels every round
                 partner = self._global(self.rank ^ step)
                 ops = [dist.P2POp(dist.isend, buf, partner, self.group), dist.P2POp(dist.irecv, recv, partner, self.group)]
                 for req in dist.batch_isend_irecv(ops):

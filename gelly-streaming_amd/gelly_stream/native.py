@@ -57,7 +57,7 @@ _SIGS = {
     "gcc_gen_host": (c_int, [POINTER(GenParams), c_uint64, c_uint64, c_void_p]),
     "gcc_gen_device": (c_int, [POINTER(GenParams), c_uint64, c_uint64, c_void_p, c_void_p]),
     "gcc_forest_create": (c_int, [c_int, c_uint32, POINTER(c_void_p)]),
-    "gcc_forest_create_ext": (c_int, [c_int, c_uint32, c_void_p, POINTER(c_void_p)]),
+    "gcc_forest_create_ext": (c_int, [c_int, c_uint32, c_void_p, c_void_p, POINTER(c_void_p)]),
     "gcc_forest_destroy": (c_int, [c_void_p]),
     "gcc_forest_set_stream": (c_int, [c_void_p, c_void_p]),
     "gcc_forest_get_stream": (c_int, [c_void_p, POINTER(c_void_p)]),
@@ -77,6 +77,7 @@ _SIGS = {
     "gcc_forest_compress": (c_int, [c_void_p]),
     "gcc_forest_labels": (c_int, [c_void_p, c_void_p, c_uint32]),
     "gcc_forest_find": (c_int, [c_void_p, c_uint32, POINTER(c_uint32)]),
+    "gcc_forest_raw_parent": (c_int, [c_void_p, c_void_p, c_uint32]),
     "gcc_forest_size": (c_int, [c_void_p, POINTER(c_uint64)]),
     "gcc_forest_count_components": (c_int, [c_void_p, POINTER(c_uint64)]),
     "gcc_forest_import_pairs": (c_int, [c_void_p, c_void_p, c_uint64]),
@@ -87,10 +88,22 @@ _SIGS = {
 _lib = None
 
 
+def _bind_torch_runtime_first() -> None:
+    """One HIP runtime per process: torch ships its own libamdhip64 / libhsa-runtime64 (same soname as
+    /opt/rocm's). If libgelly_cc were loaded first, torch would map a second HIP + HSA runtime and see no GPU
+    (measured on the MI355X box: tools/probe_runtime.py). Importing torch first makes libgelly_cc bind to the
+    already-loaded runtime by soname. Processes without torch (C/C++/JNI consumers) use /opt/rocm's."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib() -> ctypes.CDLL:
     """Load libgelly_cc.so (once). Raises GellyCCError if it has not been built."""
     global _lib
     if _lib is None:
+        _bind_torch_runtime_first()
         if not os.path.exists(LIB_PATH):
             raise GellyCCError(-3, "load", f"{LIB_PATH} not found: build it first (__graft_entry__.build())")
         l = ctypes.CDLL(LIB_PATH)

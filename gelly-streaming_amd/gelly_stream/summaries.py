@@ -59,18 +59,20 @@ class DisjointSet:
     """GPU union-find forest with the method surface of DisjointSet<R> (DisjointSet.java:30-154)."""
 
     def __init__(self, id_capacity: int, device: int = 0, elements: Optional[Iterable[int]] = None,
-                 d_parent: Optional[int] = None):
+                 d_buffers: Optional[tuple[int, int]] = None):
         """``new DisjointSet<>()`` (:36-39) / ``new DisjointSet<>(Set<R> elements)`` (:41-47).
 
-        d_parent: optional caller-owned device buffer of id_capacity u32 (e.g. a torch tensor's data_ptr()).
+        d_buffers: optional two caller-owned device buffers of id_capacity u32 each (e.g. torch tensors'
+        data_ptr()); the forest and its compressed labels alternate between them (see device_ptr()).
         """
         self.id_capacity = int(id_capacity)
         self.device = int(device)
         h = c_void_p()
-        if d_parent is None:
+        if d_buffers is None:
             call("gcc_forest_create", self.device, self.id_capacity, byref(h))
         else:
-            call("gcc_forest_create_ext", self.device, self.id_capacity, c_void_p(d_parent), byref(h))
+            call("gcc_forest_create_ext", self.device, self.id_capacity, c_void_p(d_buffers[0]),
+                 c_void_p(d_buffers[1]), byref(h))
         self._h = h
         self._labels_cache: Optional[np.ndarray] = None
         if elements is not None:
@@ -177,7 +179,7 @@ class DisjointSet:
         self._dirty()
 
     def compress(self) -> None:
-        """Canonicalise in place (async): afterwards device_ptr() holds min-id labels."""
+        """Canonicalise (async): afterwards device_ptr() holds the min-id labels."""
         call("gcc_forest_compress", self.handle)
 
     def labels(self) -> np.ndarray:
@@ -187,6 +189,12 @@ class DisjointSet:
             call("gcc_forest_labels", self.handle, out.ctypes.data, self.id_capacity)
             self._labels_cache = out
         return self._labels_cache
+
+    def raw_parent(self) -> np.ndarray:
+        """The device parent array as it stands (no compress) — for forest-invariant checks."""
+        out = np.empty(self.id_capacity, dtype=np.uint32)
+        call("gcc_forest_raw_parent", self.handle, out.ctypes.data, self.id_capacity)
+        return out
 
     def reset(self) -> None:
         """Back to the empty initial value (Merger transientState reset, SummaryAggregation.java:113-115)."""
@@ -205,6 +213,7 @@ class DisjointSet:
         return s.value or 0
 
     def device_ptr(self) -> int:
+        """The buffer currently holding the forest (after compress(): the canonical labels)."""
         p = c_void_p()
         call("gcc_forest_device_ptr", self.handle, byref(p))
         return p.value

@@ -81,13 +81,15 @@ int gcc_gen_device(const gcc_gen_params* p, uint64_t first, uint64_t count, uint
 
 /* ---- forest lifetime: `new DisjointSet<>()` (DisjointSet.java:36-39) ---- */
 int gcc_forest_create(int device, uint32_t id_capacity, gcc_forest** out);
-/* same, over caller-owned device memory of id_capacity u32 (e.g. a torch tensor); not freed by destroy */
-int gcc_forest_create_ext(int device, uint32_t id_capacity, uint32_t* d_parent, gcc_forest** out);
+/* same, over two caller-owned device buffers of id_capacity u32 each (e.g. torch tensors; not freed by
+ * destroy). The forest works in one and compress writes the canonical labels into the other, after which they
+ * swap roles: gcc_forest_device_ptr tells which one currently holds the forest / labels. */
+int gcc_forest_create_ext(int device, uint32_t id_capacity, uint32_t* d_buf0, uint32_t* d_buf1, gcc_forest** out);
 int gcc_forest_destroy(gcc_forest* h);
 int gcc_forest_set_stream(gcc_forest* h, void* hip_stream); /* NULL = the handle's own stream */
 int gcc_forest_get_stream(gcc_forest* h, void** hip_stream);
 int gcc_forest_capacity(gcc_forest* h, uint32_t* id_capacity);
-int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent); /* parent / label array, id_capacity u32 */
+int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent); /* current forest (= labels after compress) */
 /* back to the initial value (SummaryAggregation.Merger transientState reset, :113-115; fresh fold value) */
 int gcc_forest_reset(gcc_forest* h);
 
@@ -108,9 +110,11 @@ int gcc_forest_merge(gcc_forest* into, gcc_forest* from); /* into := into ∪ fr
 int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, uint32_t n);
 
 /* ---- summary reads (DisjointSet.find :71-85, getMatches :49-51; the emitted summary per window) ---- */
-int gcc_forest_compress(gcc_forest* h); /* async: parent[v] := canonical label; device array becomes labels */
+int gcc_forest_compress(gcc_forest* h); /* async: canonical labels; afterwards gcc_forest_device_ptr = labels */
 int gcc_forest_labels(gcc_forest* h, uint32_t* out, uint32_t n); /* compress + copy n labels to host */
 int gcc_forest_find(gcc_forest* h, uint32_t v, uint32_t* root); /* canonical root; GCC_UNSEEN = Java null */
+/* the raw parent array as it stands (no compress): diagnostics and tests of forest invariants */
+int gcc_forest_raw_parent(gcc_forest* h, uint32_t* out, uint32_t n);
 int gcc_forest_size(gcc_forest* h, uint64_t* n_seen);            /* getMatches().size() */
 int gcc_forest_count_components(gcc_forest* h, uint64_t* n_components);
 /* restore / deserialize: fold (key, parent) pairs (Merger.restoreState :132-135 + Kryo path) */

@@ -277,7 +277,7 @@ def test_single_edge_staging_path_crosses_batches():
     """Per-edge foldEdges calls (the Java drop-in pattern) staged in pinned memory across several batches."""
     V = 1 << 12
     rng = np.random.default_rng(3)
-    pairs = rng.integers(0, V, size=(1 << 21) + 17, dtype=np.uint32).reshape(-1, 2)  # > one staging slot
+    pairs = rng.integers(0, V, size=((1 << 20) + 17, 2), dtype=np.uint32)  # > one staging slot
     ds = DisjointSet(V)
     for u, v in pairs[:5000]:
         ds.union(int(u), int(v))
