@@ -59,7 +59,7 @@ _SIGS = {
     "gcc_forest_create": (c_int, [c_int, c_uint32, POINTER(c_void_p)]),
     "gcc_forest_create_ext": (c_int, [c_int, c_uint32, c_void_p, c_void_p, POINTER(c_void_p)]),
     "gcc_forest_destroy": (c_int, [c_void_p]),
-    "gcc_forest_set_stream": (c_int, [c_void_p, c_void_p]),
+    "gcc_forest_set_stream": (c_int, [c_void_p, c_void_p, c_int]),
     "gcc_forest_get_stream": (c_int, [c_void_p, POINTER(c_void_p)]),
     "gcc_forest_capacity": (c_int, [c_void_p, POINTER(c_uint32)]),
     "gcc_forest_device_ptr": (c_int, [c_void_p, POINTER(c_void_p)]),
@@ -83,6 +83,8 @@ _SIGS = {
     "gcc_forest_import_pairs": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_forest_enable_timing": (c_int, [c_void_p, c_int]),
     "gcc_forest_last_fold_ms": (c_int, [c_void_p, POINTER(c_float)]),
+    "gcc_forest_fold_profile": (c_int, [c_void_p, c_char_p, c_uint64]),
+    "gcc_forest_tune": (c_int, [c_void_p, c_char_p, ctypes.c_double]),
 }
 
 _lib = None

@@ -204,8 +204,9 @@ class DisjointSet:
     def sync(self) -> None:
         call("gcc_forest_sync", self.handle)
 
-    def set_stream(self, hip_stream: int) -> None:
-        call("gcc_forest_set_stream", self.handle, c_void_p(hip_stream))
+    def set_stream(self, hip_stream: Optional[int]) -> None:
+        """Order this forest's work on hip_stream (0 = the null stream); None = back to its own stream."""
+        call("gcc_forest_set_stream", self.handle, c_void_p(hip_stream or 0), 1 if hip_stream is None else 0)
 
     def stream(self) -> int:
         s = c_void_p()
@@ -230,13 +231,30 @@ class DisjointSet:
         seen = np.flatnonzero(lab != UNSEEN).astype(np.uint32)
         return np.stack([seen, lab[seen]], axis=1)
 
-    def enable_timing(self, on: bool = True) -> None:
-        call("gcc_forest_enable_timing", self.handle, 1 if on else 0)
+    def enable_timing(self, mode: int = 1) -> None:
+        """0 off; 1 HIP events around each fold and its phases; 2 also count slow-path edges."""
+        call("gcc_forest_enable_timing", self.handle, int(mode))
 
     def last_fold_ms(self) -> float:
         ms = ctypes.c_float()
         call("gcc_forest_last_fold_ms", self.handle, byref(ms))
         return ms.value
+
+    def fold_profile(self) -> list[tuple[str, float, int]]:
+        """Drain the per-phase (name, ms, edges) log of every fold since the last call (timing mode); each fold
+        starts with a ("begin", 0, 0) row (+ ("slow_edges", 0, n) rows in mode 2)."""
+        buf = ctypes.create_string_buffer(1 << 20)
+        call("gcc_forest_fold_profile", self.handle, buf, len(buf))
+        out = []
+        for line in buf.value.decode().splitlines():
+            k, ms, n = line.split()
+            out.append((k, float(ms), int(n)))
+        return out
+
+    def tune(self, **knobs) -> None:
+        """Fold-pipeline tuning (speed only; results are independent of it)."""
+        for k, v in knobs.items():
+            call("gcc_forest_tune", self.handle, k.encode(), float(v))
 
     def copy(self) -> "DisjointSet":
         """A fresh forest with the same partition (Flink copies the fold's initial value per window)."""

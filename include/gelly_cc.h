@@ -86,7 +86,9 @@ int gcc_forest_create(int device, uint32_t id_capacity, gcc_forest** out);
  * swap roles: gcc_forest_device_ptr tells which one currently holds the forest / labels. */
 int gcc_forest_create_ext(int device, uint32_t id_capacity, uint32_t* d_buf0, uint32_t* d_buf1, gcc_forest** out);
 int gcc_forest_destroy(gcc_forest* h);
-int gcc_forest_set_stream(gcc_forest* h, void* hip_stream); /* NULL = the handle's own stream */
+/* order the handle's work on hip_stream (taken literally: NULL = the null stream, e.g. torch's default
+ * stream), or back on the handle's own non-blocking stream if use_own != 0 */
+int gcc_forest_set_stream(gcc_forest* h, void* hip_stream, int use_own);
 int gcc_forest_get_stream(gcc_forest* h, void** hip_stream);
 int gcc_forest_capacity(gcc_forest* h, uint32_t* id_capacity);
 int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent); /* current forest (= labels after compress) */
@@ -121,8 +123,15 @@ int gcc_forest_count_components(gcc_forest* h, uint64_t* n_components);
 int gcc_forest_import_pairs(gcc_forest* h, const uint32_t* pairs, uint64_t n_pairs);
 
 /* ---- measurement: duration of the last fold launch (HIP events on the handle's stream) ---- */
-int gcc_forest_enable_timing(gcc_forest* h, int enable);
+int gcc_forest_enable_timing(gcc_forest* h, int enable); /* 0 off, 1 events, 2 events + slow-edge counts */
 int gcc_forest_last_fold_ms(gcc_forest* h, float* ms);
+/* measurement only (timing mode): drains the per-phase event log of every fold since the last call, as
+ * "phase ms edges" lines; each fold starts with a "begin" line (+ "slow_edges 0 n" lines in mode 2).
+ * Recording never synchronises, so a timed region stays sync-free; this call synchronises. */
+int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size);
+/* fold-pipeline tuning knobs (filter, filter_min_batch, sample_first, sample_growth, sample_div,
+ * refresh_min_batch, refresh1..refresh3); results never depend on them, only speed does */
+int gcc_forest_tune(gcc_forest* h, const char* key, double value);
 
 #ifdef __cplusplus
 }

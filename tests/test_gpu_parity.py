@@ -321,6 +321,6 @@ def test_fold_timing_events():
     cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=16, n_edges=1 << 20)
     E, V = cfg.info()
     ds = DisjointSet(V)
-    ds.enable_timing(True)
+    ds.enable_timing(1)
     ds.fold(G.generate_host(cfg))
     assert ds.last_fold_ms() > 0.0

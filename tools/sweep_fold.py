@@ -1,0 +1,60 @@
+"""GPU sweep of the fold-pipeline tuning knobs on one workload: per-phase medians, slow-path edges, parity.
+Usage: python tools/sweep_fold.py [workload] [reps]"""
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "gelly-streaming_amd"), os.path.join(ROOT, "oracle")]
+import torch  # noqa: E402
+
+import oracle as orc  # noqa: E402
+from gelly_stream import DisjointSet  # noqa: E402
+from gelly_stream import generators as G  # noqa: E402
+
+CONFIGS = [
+    ("s32_r4", {"sample_div": 32, "refresh1": 1 / 4}),
+    ("s32_r4_f2k_g8", {"sample_div": 32, "refresh1": 1 / 4, "sample_first": 2048, "sample_growth": 8}),
+    ("s32_r4_f4k_g16", {"sample_div": 32, "refresh1": 1 / 4, "sample_first": 4096, "sample_growth": 16}),
+    ("s32_r4_f8k_g8", {"sample_div": 32, "refresh1": 1 / 4, "sample_first": 8192, "sample_growth": 8}),
+    ("s32_r4_f1k_g8", {"sample_div": 32, "refresh1": 1 / 4, "sample_first": 1024, "sample_growth": 8}),
+    ("s64_r16_4_f2k_g8", {"sample_div": 64, "refresh1": 1 / 16, "refresh2": 1 / 4, "sample_first": 2048, "sample_growth": 8}),
+    ("s128_r16_4_f2k_g8", {"sample_div": 128, "refresh1": 1 / 16, "refresh2": 1 / 4, "sample_first": 2048, "sample_growth": 8}),
+]
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "c2_rmat20"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+    cfg = G.CONFIGS[wl]
+    E, V = cfg.info()
+    d = torch.empty(2 * E, dtype=torch.int32, device="cuda:0")
+    G.generate_device(cfg, 0, E, d.data_ptr(), 0)
+    torch.cuda.synchronize()
+    t = time.time()
+    want = orc.label_digest(orc.cc_stream(G.generate_host(cfg), [0, E], V, partitions=8, threads=8, want_labels=True)["labels"][0])
+    print(f"{wl}: E={E} V={V} oracle digest in {time.time() - t:.1f}s", flush=True)
+    for name, knobs in CONFIGS:
+        ds = DisjointSet(V)
+        ds.tune(**knobs)
+        ds.enable_timing(2)
+        tot, phases, ok = [], {}, True
+        for r in range(reps):
+            ds.reset()
+            ds.fold_device(d.data_ptr(), E)
+            ms = ds.last_fold_ms()
+            prof = ds.fold_profile()
+            ok &= orc.label_digest(ds.labels()) == want
+            tot.append(ms)
+            prof = [p for p in prof if p[0] != "begin"]
+            for i, (k, v, _n) in enumerate(prof):
+                phases.setdefault(f"{i}:{k}", []).append(v)
+        med = statistics.median(tot)
+        ph = " ".join(f"{k.split(':')[1]}={statistics.median(v):.3f}" for k, v in phases.items())
+        print(f"{name:18s} fold {med:.3f} ms ({E / med / 1e6:.1f} Gedge/s) {'OK' if ok else 'BAD'} | {ph}", flush=True)
+        ds.close()
+
+
+if __name__ == "__main__":
+    main()
