@@ -14,13 +14,11 @@ from gelly_stream import DisjointSet  # noqa: E402
 from gelly_stream import generators as G  # noqa: E402
 
 CONFIGS = [
-    ("s32_r4", {"sample_div": 32, "refresh1": 1 / 4}),
-    ("s32_r4_f2k_g8", {"sample_div": 32, "refresh1": 1 / 4, "sample_first": 2048, "sample_growth": 8}),
-    ("s32_r4_f4k_g16", {"sample_div": 32, "refresh1": 1 / 4, "sample_first": 4096, "sample_growth": 16}),
-    ("s32_r4_f8k_g8", {"sample_div": 32, "refresh1": 1 / 4, "sample_first": 8192, "sample_growth": 8}),
-    ("s32_r4_f1k_g8", {"sample_div": 32, "refresh1": 1 / 4, "sample_first": 1024, "sample_growth": 8}),
-    ("s64_r16_4_f2k_g8", {"sample_div": 64, "refresh1": 1 / 16, "refresh2": 1 / 4, "sample_first": 2048, "sample_growth": 8}),
-    ("s128_r16_4_f2k_g8", {"sample_div": 128, "refresh1": 1 / 16, "refresh2": 1 / 4, "sample_first": 2048, "sample_growth": 8}),
+    ("default", {}),
+    ("nofilter", {"filter": 0}),
+    ("s64_r16_4", {"sample_div": 64, "refresh1": 1 / 16, "refresh2": 1 / 4}),
+    ("s16_r4", {"sample_div": 16, "refresh1": 1 / 4}),
+    ("s32_r8_2", {"sample_div": 32, "refresh1": 1 / 8, "refresh2": 1 / 2}),
 ]
 
 
