@@ -49,19 +49,17 @@ def rank_stream(cfg, world):
     return cfg, E1, V
 
 
-def traffic_from_profiles(workload, n_edges):
-    """HBM bytes per fold launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json), or None."""
+def profile_record(workload):
+    """The newest committed rocprofv3 PMC summary for this workload (profiles/*_pmc_<workload>.json), or None."""
     pdir = os.path.join(ROOT, "profiles")
     best = None
     if os.path.isdir(pdir):
         for f in sorted(os.listdir(pdir)):
-            if f.endswith(".json") and "pmc" in f and workload in f:
+            if f.endswith(f"_pmc_{workload}.json"):
                 try:
-                    d = json.load(open(os.path.join(pdir, f)))
+                    best = json.load(open(os.path.join(pdir, f)))
                 except Exception:
                     continue
-                if d.get("n_edges") == n_edges and d.get("hbm_bytes_per_launch"):
-                    best = d
     return best
 
 
@@ -176,17 +174,26 @@ def main():
     avg_fold_edges = sum(fold_edges) / len(fold_edges)
     pipeline_gbs = BYTES_PER_EDGE * avg_fold_edges / avg_fold_s / 1e9
 
-    # per-phase events of every timed fold: the dominant phase is the kernel the roofline is quoted for
-    phases = {}
-    for name, ms, n in forest.ds.fold_profile():
-        if name != "begin":
-            phases.setdefault(name, []).append((ms, n))
-    dominant = max(phases, key=lambda k: sum(ms for ms, _ in phases[k]))
-    dom_ms = sum(ms for ms, _ in phases[dominant]) / len(phases[dominant])
-    dom_edges = sum(n for _, n in phases[dominant]) / len(phases[dominant])
+    # per-phase HIP events of every timed fold (one launch per phase entry), grouped by kernel
     kernel_of = {"filtered": "fold_filtered_kernel", "sample": "fold_kernel", "plain": "fold_kernel",
                  "refresh": "compress_bits_kernel"}
+    phases, kernels = {}, {}
+    for name, ms, n in forest.ds.fold_profile():
+        if name == "begin":
+            continue
+        phases.setdefault(name, []).append((ms, n))
+        kernels.setdefault(kernel_of.get(name, name), []).append((ms, n))
+    prof = profile_record(args.workload)
+    # the dominant kernel: the one the committed rocprof summary names for this workload, else the largest total
+    dominant = next((k for k in kernels if prof and k in prof.get("kernel", "")), None)
+    if dominant is None:
+        dominant = max(kernels, key=lambda k: sum(ms for ms, _ in kernels[k] if k != "compress_bits_kernel"))
+    dom_ms = sum(ms for ms, _ in kernels[dominant]) / len(kernels[dominant])
+    dom_edges = sum(n for _, n in kernels[dominant]) / len(kernels[dominant])
     achieved = BYTES_PER_EDGE * dom_edges / (dom_ms / 1e3) / 1e9 if dom_edges else 0.0
+    traffic = None
+    if prof and dominant in prof.get("kernel", "") and abs(prof.get("edges_per_launch", 0) - dom_edges) <= 0.01 * dom_edges:
+        traffic = prof["hbm_bytes_per_launch"]
 
     labels = forest.ds.labels()
     seen = int(np.count_nonzero(labels != 0xFFFFFFFF))
@@ -198,7 +205,6 @@ def main():
         return
 
     total_edges = world * E1 * args.steps
-    prof = traffic_from_profiles(args.workload, int(dom_edges))
     result = {
         "metric": "edges/sec into CC summary",
         "value": total_edges / elapsed,
@@ -228,17 +234,19 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": kernel_of.get(dominant, dominant),
+            "kernel": dominant,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": prof["hbm_bytes_per_launch"] if prof else None,
-            "traffic_source": prof["source"] if prof else None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch",
+            "traffic_source": (prof["source"] + f"; L2 hit rate {prof['l2_hit_rate']:.2f}") if traffic else None,
             "kernel_ms_avg": dom_ms,
             "kernel_edges_per_launch": int(dom_edges),
             "bytes_per_edge": BYTES_PER_EDGE,
             "phases_ms_per_step": {k: sum(ms for ms, _ in v) / args.steps for k, v in phases.items()},
+            "kernel_launches_per_step": len(kernels[dominant]) / args.steps,
             "pipeline": {"fold_ms_avg": avg_fold_s * 1e3, "edges_per_fold": int(avg_fold_edges),
                          "achieved": pipeline_gbs, "frac": pipeline_gbs / HBM_PEAK_GBS,
                          "host_enqueue_ms_avg": sum(host_fold_s) / len(host_fold_s) * 1e3},

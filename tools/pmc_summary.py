@@ -1,0 +1,49 @@
+"""Summarise rocprofv3 PMC passes (tools/pmc_passes.sh) into profiles/<tag>_pmc_<workload>.json.
+
+HBM bytes per launch of a kernel = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: FETCH_SIZE/WRITE_SIZE are KB, and on
+gfx950 FETCH_SIZE reports half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section). The 2x is
+exact for the 16-B/lane edge stream and uncalibrated for the random 4-B parent reads (an upper estimate there).
+Usage: python tools/pmc_summary.py <pmc_dir> <workload> <kernel substring> <edges_per_launch> <out.json>"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def per_kernel(path, counter):
+    vals = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    d, workload, ksub, edges, out = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    f = per_kernel(f"{d}/fetch/run_counter_collection.csv", "FETCH_SIZE")
+    w = per_kernel(f"{d}/write/run_counter_collection.csv", "WRITE_SIZE")
+    h = per_kernel(f"{d}/hit/run_counter_collection.csv", "TCC_HIT_sum")
+    m = per_kernel(f"{d}/hit/run_counter_collection.csv", "TCC_MISS_sum")
+    name = next(k for k in f if ksub in k)
+    fetch_kb = sum(f[name]) / len(f[name])
+    write_kb = sum(w[name]) / len(w[name])
+    hit, miss = sum(h[name]) / len(h[name]), sum(m[name]) / len(m[name])
+    rec = {
+        "workload": workload,
+        "kernel": name,
+        "launches_sampled": len(f[name]),
+        "edges_per_launch": edges,
+        "fetch_size_kb": fetch_kb,
+        "write_size_kb": write_kb,
+        "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
+        "algorithmic_bytes_per_launch": 16 * edges,
+        "l2_hit_rate": hit / (hit + miss),
+        "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum,TCC_MISS_sum (separate passes), "
+                  f"bench.py --steps 5; bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch",
+    }
+    json.dump(rec, open(out, "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
