@@ -141,7 +141,7 @@ __device__ __forceinline__ void filter_edge(u32 a, u32 b, const u32* bm, u32 g, 
 
 // queue = one segment of seg_cap slots per block. After its share of the stream, every block drains its own
 // segment (the queued slow edges, still warm in its XCD's L2) before exiting: no second launch.
-template <bool LDS, int BLOCK>
+template <bool LDS, int BLOCK, int DEPTH>
 __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
                                                               u64 n_edges, const u32* __restrict__ bits, u32 nwords,
                                                               const u32* __restrict__ giant, u64* __restrict__ queue,
@@ -167,12 +167,12 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
     const u32x4* body = reinterpret_cast<const u32x4*>(edges + head);
     const u64 stride = (u64)gridDim.x * BLOCK;
     u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
-    for (; i + 3 * stride < n2; i += 4 * stride) {
-        u32x4 q[4];
+    for (; i + (DEPTH - 1) * stride < n2; i += DEPTH * stride) {
+        u32x4 q[DEPTH];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = __builtin_nontemporal_load(body + i + k * stride);
+        for (int k = 0; k < DEPTH; ++k) q[k] = __builtin_nontemporal_load(body + i + k * stride);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < DEPTH; ++k) {
             filter_edge<LDS>(q[k].x, q[k].y, bm, g, parent, seg, qc, seg_cap);
             filter_edge<LDS>(q[k].z, q[k].w, bm, g, parent, seg, qc, seg_cap);
         }
@@ -366,6 +366,7 @@ struct FoldTune {
     u64 refresh_min_batch = 1ull << 22; // batches above this refresh the giant bitmap at the refresh points
     double refresh[3] = {1.0 / 4, 0, 0};  // refresh points (fractions of the batch), increasing, 0 = unused
     bool filter = true;
+    int depth = 4;  // 16-B edge-pair loads in flight per lane in the filtered kernel (4 or 8)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 constexpr u32 kQueueCap = 1u << 24;      // slow-edge queue capacity (128 MiB); overflow unites inline
@@ -516,18 +517,31 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
         const size_t lds = ((size_t)nw * sizeof(u64) + 15) / 16 * 16;
         static bool lds_attr_set = false;  // > 64 KiB of dynamic LDS must be allowed explicitly (once per process)
         if (!lds_attr_set) {
-            HIP_TRY(hipFuncSetAttribute((const void*)fold_filtered_kernel<true, kFilterBlockLds>,
+            HIP_TRY(hipFuncSetAttribute((const void*)fold_filtered_kernel<true, kFilterBlockLds, 4>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(kLdsBitmapMaxWords * sizeof(u64))));
+            HIP_TRY(hipFuncSetAttribute((const void*)fold_filtered_kernel<true, kFilterBlockLds, 8>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)(kLdsBitmapMaxWords * sizeof(u64))));
             lds_attr_set = true;
         }
-        hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds>), dim3(h->n_cu), dim3(kFilterBlockLds), lds,
-                           h->stream, h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw + (nw & 1),
-                           h->d_giant + h->giant_slot, h->d_queue, h->d_qcount, seg_cap);
+        if (h->tune.depth == 8)
+            hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds, 8>), dim3(h->n_cu), dim3(kFilterBlockLds), lds,
+                               h->stream, h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw + (nw & 1),
+                               h->d_giant + h->giant_slot, h->d_queue, h->d_qcount, seg_cap);
+        else
+            hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds, 4>), dim3(h->n_cu), dim3(kFilterBlockLds), lds,
+                               h->stream, h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw + (nw & 1),
+                               h->d_giant + h->giant_slot, h->d_queue, h->d_qcount, seg_cap);
     } else {
-        hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock>), dim3(nblocks), dim3(kBlock), 0, h->stream, h->d_parent,
-                           edges, n, reinterpret_cast<const u32*>(h->d_bits), nw, h->d_giant + h->giant_slot, h->d_queue,
-                           h->d_qcount, seg_cap);
+        if (h->tune.depth == 8)
+            hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock, 8>), dim3(nblocks), dim3(kBlock), 0, h->stream,
+                               h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw,
+                               h->d_giant + h->giant_slot, h->d_queue, h->d_qcount, seg_cap);
+        else
+            hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock, 4>), dim3(nblocks), dim3(kBlock), 0, h->stream,
+                               h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw,
+                               h->d_giant + h->giant_slot, h->d_queue, h->d_qcount, seg_cap);
     }
     HIP_TRY(hipGetLastError());
     int rc = prof_mark(h, "filtered", n);
@@ -1079,6 +1093,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "refresh1") t.refresh[0] = value;
     else if (k == "refresh2") t.refresh[1] = value;
     else if (k == "refresh3") t.refresh[2] = value;
+    else if (k == "depth") t.depth = (int)value == 8 ? 8 : 4;
     else return set_err(GCC_E_INVALID, "unknown tuning key '%s'", key);
     return GCC_OK;
 }

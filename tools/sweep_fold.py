@@ -15,10 +15,7 @@ from gelly_stream import generators as G  # noqa: E402
 
 CONFIGS = [
     ("default", {}),
-    ("nofilter", {"filter": 0}),
-    ("s64_r16_4", {"sample_div": 64, "refresh1": 1 / 16, "refresh2": 1 / 4}),
-    ("s16_r4", {"sample_div": 16, "refresh1": 1 / 4}),
-    ("s32_r8_2", {"sample_div": 32, "refresh1": 1 / 8, "refresh2": 1 / 2}),
+    ("depth8", {"depth": 8}),
 ]
 
 
@@ -48,6 +45,14 @@ def main():
             prof = [p for p in prof if p[0] != "begin"]
             for i, (k, v, _n) in enumerate(prof):
                 phases.setdefault(f"{i}:{k}", []).append(v)
+        # steady state: the same stream folded again into the finished forest (the filter skips ~all edges)
+        re = []
+        for r in range(reps):
+            ds.fold_device(d.data_ptr(), E)
+            re.append(ds.last_fold_ms())
+            ds.fold_profile()
+        ok &= orc.label_digest(ds.labels()) == want
+        phases["9:refold"] = re
         med = statistics.median(tot)
         ph = " ".join(f"{k.split(':')[1]}={statistics.median(v):.3f}" for k, v in phases.items())
         print(f"{name:18s} fold {med:.3f} ms ({E / med / 1e6:.1f} Gedge/s) {'OK' if ok else 'BAD'} | {ph}", flush=True)
