@@ -80,7 +80,7 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;
 constexpr int kFilterBlockLds = 1024;       // one workgroup per CU holding the whole giant bitmap in LDS
-constexpr u32 kLdsBitmapMaxWords = 18432;   // 144 KiB of the CU's 160 KiB LDS -> ids < 1,179,648
+constexpr u32 kLdsBitmapMaxWords = 18176;   // 142 KiB of the CU's 160 KiB LDS (+16 KiB of rings) -> ids < 1,163,264
 constexpr unsigned kMaxGrid = 2048;         // 256 CUs x 8 resident 256-thread blocks
 
 // Fold a batch of edges (interleaved u32 pairs) into the forest: one edge per lane per iteration, 8 B/lane
@@ -105,84 +105,96 @@ __device__ __forceinline__ u32 in_c(const u32* bm, u32 v) {
     return (bm[v >> 5] >> (v & 31)) & 1u;
 }
 
-// Append a slow edge to this block's queue segment: one LDS atomic per wave (ballot + popcount), no global
-// atomic on the streaming path (a single global counter caps at ~88 appends/us chip-wide: measured 2.5 ms).
-__device__ __forceinline__ void enqueue_or_unite(bool slow, u32 a, u32 b, u32* parent, u64* seg, u32* s_count,
-                                                 u32 seg_cap) {
+// Per-wave slow-edge ring in LDS: a wave appends its slow edges (ballot + popcount, wave-uniform cursor, no
+// atomics at all) and, whenever 64 are pending, unites them one per lane right away. The slow edges' CAS /
+// find latency then overlaps the other waves' streaming instead of forming a tail after it (measured: a
+// per-block queue drained at the end left ~25 us of tail on C2; one global queue counter capped appends at
+// ~88/us).
+constexpr u32 kRing = 128;  // u64 entries per wave (1 KiB): pending stays < 64 + 64
+
+__device__ __forceinline__ void ring_push(bool slow, u32 a, u32 b, u64* ring, u32& wq, u32& wd, u32* parent) {
     const unsigned long long m = __ballot(slow);
     if (m == 0) return;
     const u32 lane = threadIdx.x & 63;
-    const u32 leader = __ffsll((long long)m) - 1;
-    u32 base = 0;
-    if (lane == leader) base = atomicAdd(s_count, (u32)__popcll(m));
-    base = __shfl(base, leader, 64);
-    if (slow) {
-        const u32 slot = base + (u32)__popcll(m & ((1ull << lane) - 1ull));
-        if (slot < seg_cap) {
-            seg[slot] = ((u64)b << 32) | a;
-        } else {  // segment full: fold it right here
-            NoCount c;
-            UF::unite(parent, a, b, c);
-        }
+    if (slow) ring[(wq + (u32)__popcll(m & ((1ull << lane) - 1ull))) & (kRing - 1)] = ((u64)b << 32) | a;
+    wq += (u32)__popcll(m);
+    if (wq - wd >= 64) {  // wave-uniform: drain one full round, one edge per lane
+        const u64 e = ring[(wd + lane) & (kRing - 1)];
+        NoCount c;
+        UF::unite(parent, (u32)e, (u32)(e >> 32), c);
+        wd += 64;
     }
 }
 
 // One edge of the filtered stream. Both ends in C: already folded, skip. One end in C: it is connected to g
-// (C's root when the bitmap was built), so union(u, v) == union(g, other end) — queued in that form, which
-// saves the drain a dependent find through the C-side endpoint. Otherwise queued as is.
+// (C's root when the bitmap was built), so union(u, v) == union(g, other end) — pushed in that form, which
+// saves the slow path a dependent find through the C-side endpoint. Otherwise pushed as is.
 template <bool LDS>
-__device__ __forceinline__ void filter_edge(u32 a, u32 b, const u32* bm, u32 g, u32* parent, u64* seg, u32* s_count,
-                                            u32 seg_cap) {
+__device__ __forceinline__ void filter_edge(bool valid, u32 a, u32 b, const u32* bm, u32 g, u64* ring, u32& wq,
+                                            u32& wd, u32* parent) {
     const u32 ia = in_c<LDS>(bm, a), ib = in_c<LDS>(bm, b);
-    const u32 x = ia ? g : a;
-    const u32 y = ib ? g : b;
-    enqueue_or_unite(!(ia & ib), x, y, parent, seg, s_count, seg_cap);
+    ring_push(valid && !(ia & ib), ia ? g : a, ib ? g : b, ring, wq, wd, parent);
 }
 
-// queue = one segment of seg_cap slots per block. After its share of the stream, every block drains its own
-// segment (the queued slow edges, still warm in its XCD's L2) before exiting: no second launch.
+// Dynamic LDS: [bitmap (LDS variant), 16-B aligned][BLOCK/64 rings of kRing u64]. slow_count[blockIdx.x] =
+// the block's slow edges (measurement).
 template <bool LDS, int BLOCK, int DEPTH>
 __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
                                                               u64 n_edges, const u32* __restrict__ bits, u32 nwords,
-                                                              const u32* __restrict__ giant, u64* __restrict__ queue,
-                                                              u32* __restrict__ seg_count, u32 seg_cap) {
-    extern __shared__ __attribute__((aligned(16))) u32 s_bits[];
-    __shared__ u32 s_count;
-    if (threadIdx.x == 0) s_count = 0;
-    if constexpr (!LDS) __syncthreads();
-    u64* seg = queue + (u64)blockIdx.x * seg_cap;
-    u32* qc = &s_count;
+                                                              const u32* __restrict__ giant,
+                                                              u32* __restrict__ slow_count) {
+    extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
+    __shared__ u32 s_slow;
+    const u32 bitmap_u32 = LDS ? nwords * 2 : 0;  // nwords = u64 words, even
+    u64* ring = reinterpret_cast<u64*>(s_dyn + bitmap_u32) + (threadIdx.x >> 6) * kRing;
     const u32* bm = bits;
+    if (threadIdx.x == 0) s_slow = 0;
     if constexpr (LDS) {
         const u32x4* src = reinterpret_cast<const u32x4*>(bits);
-        u32x4* dst = reinterpret_cast<u32x4*>(s_bits);
-        for (u32 w = threadIdx.x; w < nwords / 2; w += BLOCK) dst[w] = src[w];  // nwords = u64 words: x2 u32 / 4
-        __syncthreads();
-        bm = s_bits;
+        u32x4* dst = reinterpret_cast<u32x4*>(s_dyn);
+        for (u32 w = threadIdx.x; w < nwords / 2; w += BLOCK) dst[w] = src[w];
+        bm = s_dyn;
     }
+    __syncthreads();
     const u32 g = *giant;
+    u32 wq = 0, wd = 0;  // this wave's ring: pushed / drained (wave-uniform)
     // split the batch into an aligned body of 16-B pairs of edges and a scalar head/tail
     const u64 head = ((reinterpret_cast<uintptr_t>(edges) & 15) && n_edges) ? 1 : 0;
     const u64 n2 = (n_edges - head) / 2;
     const u32x4* body = reinterpret_cast<const u32x4*>(edges + head);
     const u64 stride = (u64)gridDim.x * BLOCK;
-    u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
-    for (; i + (DEPTH - 1) * stride < n2; i += DEPTH * stride) {
+    const u32 lane = threadIdx.x & 63;
+    // Whole waves run both loops with the same trip count (the ring cursors wq/wd must stay wave-uniform):
+    // the loops are driven by the wave's first pair index, lanes past the end are predicated off.
+    u64 base = (u64)blockIdx.x * BLOCK + (threadIdx.x - lane);
+    for (; base + 63 + (DEPTH - 1) * stride < n2; base += DEPTH * stride) {
+        const u64 i = base + lane;
         u32x4 q[DEPTH];
 #pragma unroll
         for (int k = 0; k < DEPTH; ++k) q[k] = __builtin_nontemporal_load(body + i + k * stride);
 #pragma unroll
         for (int k = 0; k < DEPTH; ++k) {
-            filter_edge<LDS>(q[k].x, q[k].y, bm, g, parent, seg, qc, seg_cap);
-            filter_edge<LDS>(q[k].z, q[k].w, bm, g, parent, seg, qc, seg_cap);
+            filter_edge<LDS>(true, q[k].x, q[k].y, bm, g, ring, wq, wd, parent);
+            filter_edge<LDS>(true, q[k].z, q[k].w, bm, g, ring, wq, wd, parent);
         }
     }
-    for (; i < n2; i += stride) {
-        const u32x4 q = __builtin_nontemporal_load(body + i);
-        filter_edge<LDS>(q.x, q.y, bm, g, parent, seg, qc, seg_cap);
-        filter_edge<LDS>(q.z, q.w, bm, g, parent, seg, qc, seg_cap);
+    for (; base < n2; base += stride) {
+        const u64 i = base + lane;
+        const bool valid = i < n2;
+        u32x4 q = {0, 0, 0, 0};
+        if (valid) q = __builtin_nontemporal_load(body + i);
+        filter_edge<LDS>(valid, q.x, q.y, bm, g, ring, wq, wd, parent);
+        filter_edge<LDS>(valid, q.z, q.w, bm, g, ring, wq, wd, parent);
     }
     NoCount c;
+    // the rest of this wave's ring (< 64 + 64 entries)
+    for (; wd < wq; wd += 64) {
+        if (lane < wq - wd) {
+            const u64 e = ring[(wd + lane) & (kRing - 1)];
+            UF::unite(parent, (u32)e, (u32)(e >> 32), c);
+        }
+    }
+    if (lane == 0 && wq) atomicAdd(&s_slow, wq);
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // scalar head / tail edges
         if (head) UF::unite(parent, (u32)edges[0], (u32)(edges[0] >> 32), c);
         if (head + 2 * n2 < n_edges) {
@@ -191,12 +203,7 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
         }
     }
     __syncthreads();
-    const u32 nq = s_count;
-    if (threadIdx.x == 0) seg_count[blockIdx.x] = nq;  // measurement (timing mode reads it)
-    for (u32 k = threadIdx.x; k < min(nq, seg_cap); k += BLOCK) {
-        const u64 e = seg[k];
-        UF::unite(parent, (u32)e, (u32)(e >> 32), c);
-    }
+    if (threadIdx.x == 0) slow_count[blockIdx.x] = s_slow;  // measurement (profile mode reads it)
 }
 
 // Merge: into ∪ {(v, labels[v])}. labels may be any parent array of a forest over the same id range
@@ -369,7 +376,6 @@ struct FoldTune {
     int depth = 4;  // 16-B edge-pair loads in flight per lane in the filtered kernel (4 or 8)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
-constexpr u32 kQueueCap = 1u << 24;      // slow-edge queue capacity (128 MiB); overflow unites inline
 
 struct gcc_forest {
     int device = 0;
@@ -389,8 +395,7 @@ struct gcc_forest {
     u32* d_giant = nullptr;
     bool has_giant = false;
     int giant_slot = 0;  // d_giant[giant_slot] = root of the tracked component as of the last refresh
-    u64* d_queue = nullptr;
-    u32* d_qcount = nullptr;
+    u32* d_qcount = nullptr;  // per-block slow-edge counts of the last filtered launch (measurement)
 
     // pinned double-buffered staging for host-fed edges (per-edge foldEdges appends here)
     static constexpr u64 kStageEdges = 1ull << 20;  // 8 MiB per slot
@@ -504,44 +509,40 @@ static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n) {
 
 static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (n == 0) return GCC_OK;
-    const u32 nw = h->nwords();
+    const u32 nw = h->nwords() + (h->nwords() & 1);  // u64 bitmap words, rounded to 16 B
     const bool lds = nw <= kLdsBitmapMaxWords;
     const u32 nblocks = lds ? (u32)h->n_cu : kMaxGrid;
-    const u32 seg_cap = kQueueCap / nblocks;
-    if (!h->d_queue) {
-        HIP_TRY(hipMalloc((void**)&h->d_queue, (size_t)kQueueCap * sizeof(u64)));
-        HIP_TRY(hipMalloc((void**)&h->d_qcount, kMaxGrid * sizeof(u32)));
-    }
+    if (!h->d_qcount) HIP_TRY(hipMalloc((void**)&h->d_qcount, kMaxGrid * sizeof(u32)));
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
     if (lds) {
-        const size_t lds = ((size_t)nw * sizeof(u64) + 15) / 16 * 16;
+        const size_t lds_bytes = (size_t)nw * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64);
         static bool lds_attr_set = false;  // > 64 KiB of dynamic LDS must be allowed explicitly (once per process)
         if (!lds_attr_set) {
+            const int max_lds = (int)(kLdsBitmapMaxWords * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64));
             HIP_TRY(hipFuncSetAttribute((const void*)fold_filtered_kernel<true, kFilterBlockLds, 4>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)(kLdsBitmapMaxWords * sizeof(u64))));
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
             HIP_TRY(hipFuncSetAttribute((const void*)fold_filtered_kernel<true, kFilterBlockLds, 8>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)(kLdsBitmapMaxWords * sizeof(u64))));
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
             lds_attr_set = true;
         }
         if (h->tune.depth == 8)
-            hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds, 8>), dim3(h->n_cu), dim3(kFilterBlockLds), lds,
-                               h->stream, h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw + (nw & 1),
-                               h->d_giant + h->giant_slot, h->d_queue, h->d_qcount, seg_cap);
+            hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds, 8>), dim3(nblocks), dim3(kFilterBlockLds),
+                               lds_bytes, h->stream, h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw,
+                               h->d_giant + h->giant_slot, h->d_qcount);
         else
-            hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds, 4>), dim3(h->n_cu), dim3(kFilterBlockLds), lds,
-                               h->stream, h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw + (nw & 1),
-                               h->d_giant + h->giant_slot, h->d_queue, h->d_qcount, seg_cap);
+            hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds, 4>), dim3(nblocks), dim3(kFilterBlockLds),
+                               lds_bytes, h->stream, h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw,
+                               h->d_giant + h->giant_slot, h->d_qcount);
     } else {
+        const size_t lds_bytes = (kBlock / 64) * kRing * sizeof(u64);
         if (h->tune.depth == 8)
-            hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock, 8>), dim3(nblocks), dim3(kBlock), 0, h->stream,
+            hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock, 8>), dim3(nblocks), dim3(kBlock), lds_bytes, h->stream,
                                h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw,
-                               h->d_giant + h->giant_slot, h->d_queue, h->d_qcount, seg_cap);
+                               h->d_giant + h->giant_slot, h->d_qcount);
         else
-            hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock, 4>), dim3(nblocks), dim3(kBlock), 0, h->stream,
+            hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock, 4>), dim3(nblocks), dim3(kBlock), lds_bytes, h->stream,
                                h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw,
-                               h->d_giant + h->giant_slot, h->d_queue, h->d_qcount, seg_cap);
+                               h->d_giant + h->giant_slot, h->d_qcount);
     }
     HIP_TRY(hipGetLastError());
     int rc = prof_mark(h, "filtered", n);
@@ -801,7 +802,6 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (h->d_scratch) (void)hipFree(h->d_scratch);
     if (h->d_bits) (void)hipFree(h->d_bits);
     if (h->d_giant) (void)hipFree(h->d_giant);
-    if (h->d_queue) (void)hipFree(h->d_queue);
     if (h->d_qcount) (void)hipFree(h->d_qcount);
     if (h->d_counts) (void)hipFree(h->d_counts);
     for (auto& pe : h->prof) (void)hipEventDestroy(pe.second);

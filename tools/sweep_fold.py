@@ -20,8 +20,11 @@ CONFIGS = [
 
 
 def main():
+    global CONFIGS
     wl = sys.argv[1] if len(sys.argv) > 1 else "c2_rmat20"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+    if len(sys.argv) > 3:  # only the named configs
+        CONFIGS = [c for c in CONFIGS if c[0] in sys.argv[3].split(",")]
     cfg = G.CONFIGS[wl]
     E, V = cfg.info()
     d = torch.empty(2 * E, dtype=torch.int32, device="cuda:0")
@@ -50,7 +53,9 @@ def main():
         for r in range(reps):
             ds.fold_device(d.data_ptr(), E)
             re.append(ds.last_fold_ms())
-            ds.fold_profile()
+            for k, v, n in ds.fold_profile():
+                if k != "begin":
+                    phases.setdefault(f"9{len(k)}:re_{k}", []).append(v)
         ok &= orc.label_digest(ds.labels()) == want
         phases["9:refold"] = re
         med = statistics.median(tot)
