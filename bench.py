@@ -175,7 +175,8 @@ def main():
     pipeline_gbs = BYTES_PER_EDGE * avg_fold_edges / avg_fold_s / 1e9
 
     # per-phase HIP events of every timed fold (one launch per phase entry), grouped by kernel
-    kernel_of = {"filtered": "fold_filtered_kernel", "sample": "fold_kernel", "plain": "fold_kernel",
+    kernel_of = {"filtered": "fold_filtered_kernel", "sample": "fold_kernel", "plain": "fold_kernel", "seed_hub": "seed_hub_kernel",
+                 "seed_bfs": "seed_bfs_kernel", "seed_init": "seed_init_kernel",
                  "refresh": "compress_bits_kernel"}
     phases, kernels = {}, {}
     for name, ms, n in forest.ds.fold_profile():

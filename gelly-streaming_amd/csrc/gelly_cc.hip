@@ -77,6 +77,7 @@ using gcc::Count;
 using gcc::NoCount;
 typedef gcc::UnionFind<gcc::LoadPlain, true> UF;
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+typedef uint8_t u8;
 
 constexpr int kBlock = 256;
 constexpr int kFilterBlockLds = 1024;       // one workgroup per CU holding the whole giant bitmap in LDS
@@ -112,17 +113,21 @@ __device__ __forceinline__ u32 in_c(const u32* bm, u32 v) {
 // ~88/us).
 constexpr u32 kRing = 128;  // u64 entries per wave (1 KiB): pending stays < 64 + 64
 
-__device__ __forceinline__ void ring_push(bool slow, u32 a, u32 b, u64* ring, u32& wq, u32& wd, u32* parent) {
+__device__ __forceinline__ void ring_push(bool slow, u32 a, u32 b, u64* ring, u32& wq, u32& wd, u32* parent,
+                                          u32 drain_at) {
     const unsigned long long m = __ballot(slow);
     if (m == 0) return;
     const u32 lane = threadIdx.x & 63;
     if (slow) ring[(wq + (u32)__popcll(m & ((1ull << lane) - 1ull))) & (kRing - 1)] = ((u64)b << 32) | a;
     wq += (u32)__popcll(m);
-    if (wq - wd >= 64) {  // wave-uniform: drain one full round, one edge per lane
-        const u64 e = ring[(wd + lane) & (kRing - 1)];
-        NoCount c;
-        UF::unite(parent, (u32)e, (u32)(e >> 32), c);
-        wd += 64;
+    const u32 pending = wq - wd;
+    if (pending >= drain_at) {  // wave-uniform: drain one round (up to 64 edges), one edge per lane
+        if (lane < pending) {
+            const u64 e = ring[(wd + lane) & (kRing - 1)];
+            NoCount c;
+            UF::unite(parent, (u32)e, (u32)(e >> 32), c);
+        }
+        wd += pending < 64 ? pending : 64;
     }
 }
 
@@ -131,18 +136,18 @@ __device__ __forceinline__ void ring_push(bool slow, u32 a, u32 b, u64* ring, u3
 // saves the slow path a dependent find through the C-side endpoint. Otherwise pushed as is.
 template <bool LDS>
 __device__ __forceinline__ void filter_edge(bool valid, u32 a, u32 b, const u32* bm, u32 g, u64* ring, u32& wq,
-                                            u32& wd, u32* parent) {
+                                            u32& wd, u32* parent, u32 drain_at) {
     const u32 ia = in_c<LDS>(bm, a), ib = in_c<LDS>(bm, b);
-    ring_push(valid && !(ia & ib), ia ? g : a, ib ? g : b, ring, wq, wd, parent);
+    ring_push(valid && !(ia & ib), ia ? g : a, ib ? g : b, ring, wq, wd, parent, drain_at);
 }
 
 // Dynamic LDS: [bitmap (LDS variant), 16-B aligned][BLOCK/64 rings of kRing u64]. slow_count[blockIdx.x] =
 // the block's slow edges (measurement).
-template <bool LDS, int BLOCK, int DEPTH>
+template <bool LDS, int BLOCK, int DEPTH, bool PIPE>
 __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
                                                               u64 n_edges, const u32* __restrict__ bits, u32 nwords,
                                                               const u32* __restrict__ giant,
-                                                              u32* __restrict__ slow_count) {
+                                                              u32* __restrict__ slow_count, u32 drain_at) {
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     __shared__ u32 s_slow;
     const u32 bitmap_u32 = LDS ? nwords * 2 : 0;  // nwords = u64 words, even
@@ -167,15 +172,43 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
     // Whole waves run both loops with the same trip count (the ring cursors wq/wd must stay wave-uniform):
     // the loops are driven by the wave's first pair index, lanes past the end are predicated off.
     u64 base = (u64)blockIdx.x * BLOCK + (threadIdx.x - lane);
-    for (; base + 63 + (DEPTH - 1) * stride < n2; base += DEPTH * stride) {
-        const u64 i = base + lane;
-        u32x4 q[DEPTH];
+    if constexpr (PIPE) {
+        // software-pipelined: the next DEPTH loads are in flight while this round is filtered (and while a
+        // ring drain waits on its union chains)
+        if (base + 63 + (DEPTH - 1) * stride < n2) {
+            u32x4 q[DEPTH];
 #pragma unroll
-        for (int k = 0; k < DEPTH; ++k) q[k] = __builtin_nontemporal_load(body + i + k * stride);
+            for (int k = 0; k < DEPTH; ++k) q[k] = __builtin_nontemporal_load(body + base + lane + k * stride);
+            while (true) {
+                const u64 nb = base + DEPTH * stride;
+                const bool more = nb + 63 + (DEPTH - 1) * stride < n2;  // wave-uniform
+                u32x4 nq[DEPTH];
+                if (more) {
 #pragma unroll
-        for (int k = 0; k < DEPTH; ++k) {
-            filter_edge<LDS>(true, q[k].x, q[k].y, bm, g, ring, wq, wd, parent);
-            filter_edge<LDS>(true, q[k].z, q[k].w, bm, g, ring, wq, wd, parent);
+                    for (int k = 0; k < DEPTH; ++k) nq[k] = __builtin_nontemporal_load(body + nb + lane + k * stride);
+                }
+#pragma unroll
+                for (int k = 0; k < DEPTH; ++k) {
+                    filter_edge<LDS>(true, q[k].x, q[k].y, bm, g, ring, wq, wd, parent, drain_at);
+                    filter_edge<LDS>(true, q[k].z, q[k].w, bm, g, ring, wq, wd, parent, drain_at);
+                }
+                base = nb;
+                if (!more) break;
+#pragma unroll
+                for (int k = 0; k < DEPTH; ++k) q[k] = nq[k];
+            }
+        }
+    } else {
+        for (; base + 63 + (DEPTH - 1) * stride < n2; base += DEPTH * stride) {
+            const u64 i = base + lane;
+            u32x4 q[DEPTH];
+#pragma unroll
+            for (int k = 0; k < DEPTH; ++k) q[k] = __builtin_nontemporal_load(body + i + k * stride);
+#pragma unroll
+            for (int k = 0; k < DEPTH; ++k) {
+                filter_edge<LDS>(true, q[k].x, q[k].y, bm, g, ring, wq, wd, parent, drain_at);
+                filter_edge<LDS>(true, q[k].z, q[k].w, bm, g, ring, wq, wd, parent, drain_at);
+            }
         }
     }
     for (; base < n2; base += stride) {
@@ -183,8 +216,8 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
         const bool valid = i < n2;
         u32x4 q = {0, 0, 0, 0};
         if (valid) q = __builtin_nontemporal_load(body + i);
-        filter_edge<LDS>(valid, q.x, q.y, bm, g, ring, wq, wd, parent);
-        filter_edge<LDS>(valid, q.z, q.w, bm, g, ring, wq, wd, parent);
+        filter_edge<LDS>(valid, q.x, q.y, bm, g, ring, wq, wd, parent, drain_at);
+        filter_edge<LDS>(valid, q.z, q.w, bm, g, ring, wq, wd, parent, drain_at);
     }
     NoCount c;
     // the rest of this wave's ring (< 64 + 64 entries)
@@ -313,6 +346,229 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Seeding a FRESH forest without parent[] atomics (DESIGN.md §4 "seeded fold").
+// A from-scratch fold of a skewed stream spends its time in CAS storms on the hubs' roots. Instead:
+//  (1) seed_hub_kernel: the most frequent endpoint h of the batch's first edges (LDS hash count) —
+//      on a skewed stream a hub, in the eventual giant component. Also clears the flag bytes;
+//  (2) seed_bfs_kernel (a few passes over a prefix of the batch): C := C ∪ {x} for every edge (y, x) with
+//      y ∈ C — a BFS from h over the prefix edges, on one flag byte per id. Setting a flag is an idempotent
+//      plain byte store (no atomics: a stale read only delays a flag to the next pass). Every id in C is
+//      connected to h by edges of this batch, so C lies inside one component of the folded forest;
+//      gmin = min C (block minimum, one atomicMin only when it beats the current value);
+//  (3) seed_init_kernel: parent[v] = (v ∈ C) ? gmin : UNSEEN and the bitmap of C — the reset and all of C's
+//      union work in one pass. The filtered kernel then folds the WHOLE batch against C: edges inside C are
+//      skipped, every other edge (prefix included) takes the union path, so the result is exact.
+// ------------------------------------------------------------------------------------------------
+constexpr int kHubBlock = 1024;
+constexpr u32 kHubSlots = 16384;  // LDS open-addressing table (key, count): 128 KiB, load factor <= 1/4
+constexpr u32 kHubProbe = 64;
+constexpr u64 kHubSample = 2048;  // edges sampled for the hub vote (2 per thread)
+
+__device__ __forceinline__ void hub_count(u32 x, u32* s_key, u32* s_cnt) {
+    u32 s = (u32)(gcc_splitmix64(x) & (kHubSlots - 1));
+    for (u32 p = 0; p < kHubProbe; ++p, s = (s + 1) & (kHubSlots - 1)) {
+        const u32 k = atomicCAS(&s_key[s], UNSEEN, x);
+        if (k == UNSEEN || k == x) {
+            atomicAdd(&s_cnt[s], 1u);
+            return;
+        }
+    }
+}
+
+__device__ __forceinline__ bool hub_better(u32 c, u32 k, u32 bc, u32 bk) { return c > bc || (c == bc && c && k < bk); }
+
+// Elects h and initialises C = {h}: flags (zeroed up to a whole bitmap word) and the bitmap. Every block of
+// the grid elects the same h (deterministic argmax) and clears its own share of both arrays.
+__global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restrict__ edges, u64 n_sample,
+                                                             u8* __restrict__ flags, u32* __restrict__ bits32, u32 n,
+                                                             u32* __restrict__ gmin) {
+    extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
+    u32* s_key = s_dyn;
+    u32* s_cnt = s_dyn + kHubSlots;
+    __shared__ u32 s_bc[kHubBlock / 64], s_bk[kHubBlock / 64];
+    constexpr int kPer = (int)(kHubSample / kHubBlock);
+    u64 e[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {  // all sample loads in flight at once
+        const u64 i = threadIdx.x + (u64)k * kHubBlock;
+        e[k] = i < n_sample ? edges[i] : ~0ull;
+    }
+    for (u32 s = threadIdx.x; s < kHubSlots; s += kHubBlock) {
+        s_key[s] = UNSEEN;
+        s_cnt[s] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        if (e[k] == ~0ull) continue;
+        hub_count((u32)e[k], s_key, s_cnt);
+        hub_count((u32)(e[k] >> 32), s_key, s_cnt);
+    }
+    __syncthreads();
+    // argmax over (count desc, id asc)
+    u32 bc = 0, bk = UNSEEN;
+    for (u32 s = threadIdx.x; s < kHubSlots; s += kHubBlock)
+        if (hub_better(s_cnt[s], s_key[s], bc, bk)) {
+            bc = s_cnt[s];
+            bk = s_key[s];
+        }
+    for (int off = 32; off > 0; off >>= 1) {
+        const u32 c2 = __shfl_down(bc, off, 64), k2 = __shfl_down(bk, off, 64);
+        if (hub_better(c2, k2, bc, bk)) {
+            bc = c2;
+            bk = k2;
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_bc[threadIdx.x >> 6] = bc;
+        s_bk[threadIdx.x >> 6] = bk;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kHubBlock / 64; ++w)
+            if (hub_better(s_bc[w], s_bk[w], s_bc[0], s_bk[0])) {
+                s_bc[0] = s_bc[w];
+                s_bk[0] = s_bk[w];
+            }
+    }
+    __syncthreads();
+    const u32 h = s_bk[0];  // n_sample >= 1, so some endpoint was counted
+    // this block's share: 32 ids per unit = 32 flag bytes (two 16-B stores) + one bitmap word
+    const u64 nu = ((u64)n + 31) / 32;
+    const u64 per = (nu + gridDim.x - 1) / gridDim.x;
+    const u64 u0 = blockIdx.x * per, u1 = min(nu, u0 + per);
+    u32x4* f4 = reinterpret_cast<u32x4*>(flags);
+    for (u64 u = u0 + threadIdx.x; u < u1; u += kHubBlock) {
+        u32x4 z0 = {0, 0, 0, 0}, z1 = {0, 0, 0, 0};
+        u32 w = 0;
+        if (u == h / 32) {
+            const u32 o = h & 31;
+            if (o < 16) z0[o >> 2] = 1u << (8 * (o & 3));
+            else z1[(o - 16) >> 2] = 1u << (8 * (o & 3));
+            w = 1u << o;
+        }
+        f4[2 * u] = z0;
+        f4[2 * u + 1] = z1;
+        bits32[u] = w;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *gmin = h;
+}
+
+// One BFS pass over the prefix. LDS = true: every block (one per CU) holds the bitmap of C as of the last
+// pack in LDS; a discovered id is set there too (LDS atomicOr: propagation inside the block, and each id is
+// flagged once per block), then flagged in HBM. LDS = false: lookups go to the global bitmap.
+template <bool LDS, int BLOCK, bool NT>
+__global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__ edges, u64 n,
+                                                         const u32* __restrict__ bits32, u32 nwords32,
+                                                         u8* __restrict__ flags, u32* __restrict__ gmin) {
+    extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
+    __shared__ u32 s_min;
+    u32* bm = const_cast<u32*>(bits32);
+    if (threadIdx.x == 0) s_min = UNSEEN;
+    if constexpr (LDS) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(bits32);
+        u32x4* dst = reinterpret_cast<u32x4*>(s_dyn);
+        for (u32 w = threadIdx.x; w < nwords32 / 4; w += BLOCK) dst[w] = src[w];
+        bm = s_dyn;
+    }
+    __syncthreads();
+    u32 lmin = UNSEEN;
+    auto visit = [&](u32 a, u32 b) {
+        const u32 ia = (bm[a >> 5] >> (a & 31)) & 1u, ib = (bm[b >> 5] >> (b & 31)) & 1u;
+        if (ia != ib) {
+            const u32 x = ia ? b : a, m = 1u << (x & 31);
+            bool fresh = true;
+            if constexpr (LDS) fresh = !(atomicOr(&bm[x >> 5], m) & m);
+            if (fresh) {
+                flags[x] = 1;
+                lmin = min(lmin, x);
+            }
+        }
+    };
+    auto ld = [](const u32x4* p) -> u32x4 {
+        if constexpr (NT) return __builtin_nontemporal_load(p);
+        else return *p;
+    };
+    // aligned body of 16-B edge pairs (four in flight per lane) + scalar head/tail edges
+    const u64 head = ((reinterpret_cast<uintptr_t>(edges) & 15) && n) ? 1 : 0;
+    const u64 n2 = (n - head) / 2;
+    const u32x4* body = reinterpret_cast<const u32x4*>(edges + head);
+    const u64 stride = (u64)gridDim.x * BLOCK;
+    u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+    for (; i + 3 * stride < n2; i += 4 * stride) {
+        u32x4 q[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = ld(body + i + k * stride);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            visit(q[k].x, q[k].y);
+            visit(q[k].z, q[k].w);
+        }
+    }
+    for (; i < n2; i += stride) {
+        const u32x4 q = ld(body + i);
+        visit(q.x, q.y);
+        visit(q.z, q.w);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (head) visit((u32)edges[0], (u32)(edges[0] >> 32));
+        if (head + 2 * n2 < n) visit((u32)edges[n - 1], (u32)(edges[n - 1] >> 32));
+    }
+    for (int off = 32; off > 0; off >>= 1) lmin = min(lmin, (u32)__shfl_down(lmin, off, 64));
+    if ((threadIdx.x & 63) == 0 && lmin != UNSEEN) atomicMin(&s_min, lmin);
+    __syncthreads();
+    // one global atomic only for a new record (same-address atomics serialise at the memory side)
+    if (threadIdx.x == 0 && s_min < __hip_atomic_load(gmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMin(gmin, s_min);
+}
+
+// Pack the flag bytes into the bitmap of C (8 lanes = one u32 word, 4 ids per lane). PARENT = true (the
+// last step of the seeding): also parent[v] = (v in C) ? gmin : UNSEEN with 16-B stores, and publish gmin as
+// the tracked component.
+template <bool PARENT>
+__global__ __launch_bounds__(kBlock) void seed_pack_kernel(u32* __restrict__ parent, u32 n, const u8* __restrict__ flags,
+                                                           u32* __restrict__ bits32, const u32* __restrict__ gmin,
+                                                           u32* __restrict__ giant) {
+    u32 g = 0;
+    if constexpr (PARENT) {
+        g = *gmin;
+        if (blockIdx.x == 0 && threadIdx.x == 0) *giant = g;
+    }
+    const u64 stride = (u64)gridDim.x * kBlock;
+    const u64 nq = ((u64)n + 31) / 32 * 8;  // whole bitmap words
+    const u32* f32 = reinterpret_cast<const u32*>(flags);
+    u32x4* p4 = reinterpret_cast<u32x4*>(parent);
+    const u32 lane = threadIdx.x & 63;
+    for (u64 q0 = (u64)blockIdx.x * kBlock + (threadIdx.x - lane); q0 < nq; q0 += stride) {  // whole waves
+        const u64 q = q0 + lane;
+        u32 nib = 0;
+        if (q < nq) {
+            const u32 f = f32[q];  // flag bytes of ids 4q..4q+3 (0 or 1 each)
+            nib = (f & 1u) | ((f >> 7) & 2u) | ((f >> 14) & 4u) | ((f >> 21) & 8u);
+            if constexpr (PARENT) {
+                const u64 v = 4 * q;
+                if (v + 3 < n) {
+                    u32x4 o;
+                    o.x = (nib & 1u) ? g : UNSEEN;
+                    o.y = (nib & 2u) ? g : UNSEEN;
+                    o.z = (nib & 4u) ? g : UNSEEN;
+                    o.w = (nib & 8u) ? g : UNSEEN;
+                    p4[q] = o;
+                } else {
+                    for (u32 k = 0; k < 4; ++k)
+                        if (v + k < n) parent[v + k] = ((nib >> k) & 1u) ? g : UNSEEN;
+                }
+            }
+        }
+        u32 w = nib << ((lane & 7) * 4);
+        w |= __shfl_xor(w, 1, 64);
+        w |= __shfl_xor(w, 2, 64);
+        w |= __shfl_xor(w, 4, 64);
+        if ((lane & 7) == 0 && q < nq) bits32[q >> 3] = w;
+    }
+}
+
 // counts[0] += #seen, counts[1] += #roots (= #components)
 __global__ __launch_bounds__(kBlock) void count_kernel(const u32* __restrict__ parent, u32 n,
                                                        unsigned long long* __restrict__ counts) {
@@ -374,6 +630,14 @@ struct FoldTune {
     double refresh[3] = {1.0 / 4, 0, 0};  // refresh points (fractions of the batch), increasing, 0 = unused
     bool filter = true;
     int depth = 4;  // 16-B edge-pair loads in flight per lane in the filtered kernel (4 or 8)
+    // seeded fold of a fresh forest (seed_* kernels): BFS from a hub over the first 1/seed_div of the batch
+    bool seed = true;
+    int seed_passes = 2;
+    u64 seed_div = 2;
+    double seed_refresh = 0;  // refresh point of a seeded batch (fraction; 0 = none)
+    bool pipe = true;  // software-pipelined filtered stream (next round's loads in flight during filtering)
+    u32 drain_at = 64;  // a wave drains its slow-edge ring once this many edges are pending (1..64)
+    bool seed_nt = true;  // non-temporal loads in the BFS passes (false: the prefix may stay in the MALL)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -386,13 +650,16 @@ struct gcc_forest {
     u32* d_spare = nullptr;
     bool own_bufs = true;
     bool compressed = false;  // d_parent holds canonical labels (no mutation since the last compress)
+    // reset() is lazy: the next fold of a fresh forest writes parent[] itself (seed_init_kernel); any other
+    // use materialises the all-UNSEEN forest first (materialize_reset)
+    bool pending_reset = false;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     int n_cu = 256;
 
     // giant-component filter: bitmap of one component (valid forever: components only grow)
     u64* d_bits = nullptr;
-    u32* d_giant = nullptr;
+    u32* d_giant = nullptr;  // [0], [1]: tracked-component root slots; [2]: seed gmin
     bool has_giant = false;
     int giant_slot = 0;  // d_giant[giant_slot] = root of the tracked component as of the last refresh
     u32* d_qcount = nullptr;  // per-block slow-edge counts of the last filtered launch (measurement)
@@ -459,16 +726,28 @@ static void mark_mutated(gcc_forest* h) {
     h->compressed = false;
 }
 
+static int materialize_reset(gcc_forest* h) {
+    if (!h->pending_reset) return GCC_OK;
+    HIP_TRY(hipMemsetAsync(h->d_parent, 0xFF, (size_t)h->cap * sizeof(u32), h->stream));
+    h->pending_reset = false;
+    return GCC_OK;
+}
+
+static int alloc_filter(gcc_forest* h) {
+    if (h->d_bits) return GCC_OK;
+    HIP_TRY(hipMalloc((void**)&h->d_bits, (size_t)h->nwords() * sizeof(u64) + 16));
+    HIP_TRY(hipMalloc((void**)&h->d_giant, 4 * sizeof(u32)));
+    return GCC_OK;
+}
+
 // compress into the spare buffer and swap; with the filter on, refresh the giant bitmap from the new labels
 static int compress_now(gcc_forest* h) {
     if (!h->filter_enabled()) {
         hipLaunchKernelGGL(compress_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent,
                            h->d_spare, h->cap);
     } else {
-        if (!h->d_bits) {
-            HIP_TRY(hipMalloc((void**)&h->d_bits, (size_t)h->nwords() * sizeof(u64) + 16));
-            HIP_TRY(hipMalloc((void**)&h->d_giant, 2 * sizeof(u32)));
-        }
+        int rc = alloc_filter(h);
+        if (rc) return rc;
         if (!h->has_giant)  // first refresh of this forest: elect the component to track
             hipLaunchKernelGGL(giant_vote_kernel, dim3(1), dim3(1024), 0, h->stream, h->d_parent, h->cap,
                                h->d_giant + h->giant_slot);
@@ -514,35 +793,43 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u32 nblocks = lds ? (u32)h->n_cu : kMaxGrid;
     if (!h->d_qcount) HIP_TRY(hipMalloc((void**)&h->d_qcount, kMaxGrid * sizeof(u32)));
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
+    const u32* bits = reinterpret_cast<const u32*>(h->d_bits);
+    const u32* giant = h->d_giant + h->giant_slot;
+    const int variant = (h->tune.depth == 8 ? 1 : 0) | (h->tune.pipe ? 2 : 0);
     if (lds) {
         const size_t lds_bytes = (size_t)nw * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64);
         static bool lds_attr_set = false;  // > 64 KiB of dynamic LDS must be allowed explicitly (once per process)
         if (!lds_attr_set) {
             const int max_lds = (int)(kLdsBitmapMaxWords * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64));
-            HIP_TRY(hipFuncSetAttribute((const void*)fold_filtered_kernel<true, kFilterBlockLds, 4>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
-            HIP_TRY(hipFuncSetAttribute((const void*)fold_filtered_kernel<true, kFilterBlockLds, 8>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
+            const void* fns[4] = {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, false>,
+                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, false>,
+                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true>,
+                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true>};
+            for (const void* f : fns) HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
             lds_attr_set = true;
         }
-        if (h->tune.depth == 8)
-            hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds, 8>), dim3(nblocks), dim3(kFilterBlockLds),
-                               lds_bytes, h->stream, h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw,
-                               h->d_giant + h->giant_slot, h->d_qcount);
-        else
-            hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds, 4>), dim3(nblocks), dim3(kFilterBlockLds),
-                               lds_bytes, h->stream, h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw,
-                               h->d_giant + h->giant_slot, h->d_qcount);
+#define GCC_FILTERED(D, P)                                                                                       \
+    hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds, D, P>), dim3(nblocks), dim3(kFilterBlockLds), \
+                       lds_bytes, h->stream, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
+        switch (variant) {
+        case 0: GCC_FILTERED(4, false); break;
+        case 1: GCC_FILTERED(8, false); break;
+        case 2: GCC_FILTERED(4, true); break;
+        default: GCC_FILTERED(8, true); break;
+        }
+#undef GCC_FILTERED
     } else {
         const size_t lds_bytes = (kBlock / 64) * kRing * sizeof(u64);
-        if (h->tune.depth == 8)
-            hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock, 8>), dim3(nblocks), dim3(kBlock), lds_bytes, h->stream,
-                               h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw,
-                               h->d_giant + h->giant_slot, h->d_qcount);
-        else
-            hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock, 4>), dim3(nblocks), dim3(kBlock), lds_bytes, h->stream,
-                               h->d_parent, edges, n, reinterpret_cast<const u32*>(h->d_bits), nw,
-                               h->d_giant + h->giant_slot, h->d_qcount);
+#define GCC_FILTERED(D, P)                                                                                  \
+    hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock, D, P>), dim3(nblocks), dim3(kBlock), lds_bytes, \
+                       h->stream, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
+        switch (variant) {
+        case 0: GCC_FILTERED(4, false); break;
+        case 1: GCC_FILTERED(8, false); break;
+        case 2: GCC_FILTERED(4, true); break;
+        default: GCC_FILTERED(8, true); break;
+        }
+#undef GCC_FILTERED
     }
     HIP_TRY(hipGetLastError());
     int rc = prof_mark(h, "filtered", n);
@@ -559,12 +846,84 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
     return GCC_OK;
 }
 
+// Seeded start of a fresh forest's first batch (seed_* kernels above): hub vote, BFS passes over the
+// prefix, parent[] := C ? gmin : UNSEEN. Replaces the reset memset; leaves has_giant set, bitmap = C.
+static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
+    const FoldTune& t = h->tune;
+    int rc = alloc_filter(h);
+    if (rc) return rc;
+    const u64* edges = reinterpret_cast<const u64*>(d_pairs);
+    u8* flags = reinterpret_cast<u8*>(h->d_spare);  // free until the next compress: one flag byte per id
+    u32* bits = reinterpret_cast<u32*>(h->d_bits);
+    u32* gmin = h->d_giant + 2;
+    const unsigned hub_grid = (unsigned)std::max<u64>(1, std::min<u64>((u64)h->n_cu, (u64)h->cap >> 16));
+    static bool hub_attr = false;
+    if (!hub_attr) {
+        HIP_TRY(hipFuncSetAttribute((const void*)seed_hub_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(2 * kHubSlots * sizeof(u32))));
+        hub_attr = true;
+    }
+    hipLaunchKernelGGL(seed_hub_kernel, dim3(hub_grid), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32), h->stream, edges,
+                       std::min(n, kHubSample), flags, bits, h->cap, gmin);
+    HIP_TRY(hipGetLastError());
+    rc = prof_mark(h, "seed_hub");
+    if (rc) return rc;
+    const u64 pref = std::min(n, std::max<u64>(t.filter_min_batch, n / std::max<u64>(1, t.seed_div)));
+    const u32 nw32 = 2 * (h->nwords() + (h->nwords() & 1));  // u32 bitmap words, rounded to 16 B
+    const bool lds = nw32 / 2 <= kLdsBitmapMaxWords;
+    const unsigned pack_grid = grid_for(((u64)h->cap + 3) / 4, kMaxGrid);
+    for (int p = 0; p < t.seed_passes; ++p) {
+        if (lds) {
+            static bool attr = false;
+            if (!attr) {
+                for (const void* f : {(const void*)seed_bfs_kernel<true, kFilterBlockLds, true>,
+                                      (const void*)seed_bfs_kernel<true, kFilterBlockLds, false>})
+                    HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)(kLdsBitmapMaxWords * sizeof(u64))));
+                attr = true;
+            }
+            if (t.seed_nt)
+                hipLaunchKernelGGL((seed_bfs_kernel<true, kFilterBlockLds, true>), dim3(h->n_cu), dim3(kFilterBlockLds),
+                                   (size_t)nw32 * sizeof(u32), h->stream, edges, pref, bits, nw32, flags, gmin);
+            else
+                hipLaunchKernelGGL((seed_bfs_kernel<true, kFilterBlockLds, false>), dim3(h->n_cu), dim3(kFilterBlockLds),
+                                   (size_t)nw32 * sizeof(u32), h->stream, edges, pref, bits, nw32, flags, gmin);
+        } else {
+            const unsigned grid = grid_for((pref + 1) / 2, kMaxGrid);
+            if (t.seed_nt)
+                hipLaunchKernelGGL((seed_bfs_kernel<false, kBlock, true>), dim3(grid), dim3(kBlock), 0, h->stream, edges,
+                                   pref, bits, nw32, flags, gmin);
+            else
+                hipLaunchKernelGGL((seed_bfs_kernel<false, kBlock, false>), dim3(grid), dim3(kBlock), 0, h->stream, edges,
+                                   pref, bits, nw32, flags, gmin);
+        }
+        HIP_TRY(hipGetLastError());
+        rc = prof_mark(h, "seed_bfs", pref);
+        if (rc) return rc;
+        if (p + 1 < t.seed_passes) {
+            hipLaunchKernelGGL(seed_pack_kernel<false>, dim3(pack_grid), dim3(kBlock), 0, h->stream, h->d_parent, h->cap,
+                               flags, bits, gmin, h->d_giant + h->giant_slot);
+            HIP_TRY(hipGetLastError());
+            rc = prof_mark(h, "seed_pack");
+            if (rc) return rc;
+        }
+    }
+    hipLaunchKernelGGL(seed_pack_kernel<true>, dim3(pack_grid), dim3(kBlock), 0, h->stream, h->d_parent, h->cap, flags,
+                       bits, gmin, h->d_giant + h->giant_slot);
+    HIP_TRY(hipGetLastError());
+    h->pending_reset = false;
+    h->has_giant = true;
+    return prof_mark(h, "seed_init");
+}
+
 // The fold pipeline for one batch (UpdateCC.foldEdges over the batch, DisjointSet.union per edge):
-//  1. a fresh forest first folds a sampling prefix in geometrically growing launches (4K, 16K, ... edges):
-//     few threads contend while the hubs are still unhooked, which avoids the CAS storm a single full-width
-//     launch causes on the hubs of a skewed stream (measured: 3.5-5 ms -> ~0.06 ms on C2);
+//  0. a FRESH forest (reset, nothing folded since) is seeded: launch_seed builds the component of a hub
+//     over a prefix on a bitmap and writes parent[] from it; the filtered kernel then folds the whole batch;
+//  1. otherwise a forest without a tracked component first folds a sampling prefix in geometrically growing
+//     launches (4K, 16K, ... edges): few threads contend while the hubs are still unhooked, which avoids the
+//     CAS storm a single full-width launch causes on the hubs of a skewed stream;
 //  2. compress + vote + bitmap of the giant component;
-//  3. the rest streams through the giant-filtered kernel; large batches refresh the bitmap once, at 1/8.
+//  3. the rest streams through the giant-filtered kernel; large batches refresh the bitmap at the refresh points.
 static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (n == 0) return GCC_OK;
     const FoldTune& t = h->tune;
@@ -576,6 +935,17 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
     }
     int rc = GCC_OK;
     u64 b = 0;
+    const bool seeded = h->pending_reset && h->filter_enabled() && t.seed && n >= t.filter_min_batch &&
+                        ((reinterpret_cast<uintptr_t>(h->d_parent) | reinterpret_cast<uintptr_t>(h->d_spare)) & 15) == 0;
+    double refresh[3] = {t.refresh[0], t.refresh[1], t.refresh[2]};
+    if (seeded) {
+        rc = launch_seed(h, d_pairs, n);
+        refresh[0] = t.seed_refresh;
+        refresh[1] = refresh[2] = 0;
+    } else {
+        rc = materialize_reset(h);
+    }
+    if (rc) return rc;
     if (!h->filter_enabled() || (!h->has_giant && n < t.filter_min_batch)) {
         rc = launch_plain(h, d_pairs, n);
         b = n;
@@ -595,8 +965,8 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
     while (!rc && b < n) {
         u64 e = n;
         if (n > t.refresh_min_batch) {
-            while (next_refresh < 3 && t.refresh[next_refresh] > 0 && (u64)(n * t.refresh[next_refresh]) <= b) ++next_refresh;
-            if (next_refresh < 3 && t.refresh[next_refresh] > 0) e = std::max<u64>(b + 1, (u64)(n * t.refresh[next_refresh]));
+            while (next_refresh < 3 && refresh[next_refresh] > 0 && (u64)(n * refresh[next_refresh]) <= b) ++next_refresh;
+            if (next_refresh < 3 && refresh[next_refresh] > 0) e = std::max<u64>(b + 1, (u64)(n * refresh[next_refresh]));
         }
         rc = launch_filtered(h, d_pairs + 2 * b, e - b);
         b = e;
@@ -641,9 +1011,17 @@ static int alloc_staging(gcc_forest* h) {
     return GCC_OK;
 }
 
-static int flush(gcc_forest* h) {
+// submit the staged host edges (a fold handles a pending reset itself)
+static int flush_staged(gcc_forest* h) {
     if (h->staged == 0) return GCC_OK;
     return submit_slot(h, h->staged);
+}
+
+// everything queued, and parent[] materialised: the state every non-fold entry point works on
+static int flush(gcc_forest* h) {
+    int rc = flush_staged(h);
+    if (rc) return rc;
+    return materialize_reset(h);
 }
 
 static int compress_async(gcc_forest* h) {
@@ -845,6 +1223,9 @@ int gcc_forest_capacity(gcc_forest* h, uint32_t* id_capacity) {
 
 int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent) {
     CHECK_ARG(h && d_parent, "null argument");
+    DeviceGuard g(h->device);
+    int rc = flush(h);
+    if (rc) return rc;
     *d_parent = h->d_parent;
     return GCC_OK;
 }
@@ -853,7 +1234,7 @@ int gcc_forest_reset(gcc_forest* h) {
     CHECK_ARG(h, "null forest");
     DeviceGuard g(h->device);
     h->staged = 0;
-    HIP_TRY(hipMemsetAsync(h->d_parent, 0xFF, (size_t)h->cap * sizeof(u32), h->stream));
+    h->pending_reset = true;  // materialised lazily (see gcc_forest::pending_reset)
     h->host_valid = false;
     h->compressed = true;  // all UNSEEN is canonical
     h->has_giant = false;  // the giant bitmap described the old forest
@@ -933,7 +1314,7 @@ int gcc_forest_fold_device(gcc_forest* h, const uint32_t* d_pairs, uint64_t n_ed
     CHECK_ARG(h, "null forest");
     CHECK_ARG(d_pairs || n_edges == 0, "d_pairs is null");
     DeviceGuard g(h->device);
-    int rc = flush(h);
+    int rc = flush_staged(h);
     if (rc) return rc;
     return launch_fold(h, d_pairs, n_edges);
 }
@@ -1094,6 +1475,13 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "refresh2") t.refresh[1] = value;
     else if (k == "refresh3") t.refresh[2] = value;
     else if (k == "depth") t.depth = (int)value == 8 ? 8 : 4;
+    else if (k == "seed") t.seed = value != 0;
+    else if (k == "pipe") t.pipe = value != 0;
+    else if (k == "drain_at") t.drain_at = (u32)std::max(1.0, std::min(64.0, value));
+    else if (k == "seed_nt") t.seed_nt = value != 0;
+    else if (k == "seed_passes") t.seed_passes = std::max(0, std::min(16, (int)value));
+    else if (k == "seed_div") t.seed_div = std::max<u64>(1, (u64)value);
+    else if (k == "seed_refresh") t.seed_refresh = value;
     else return set_err(GCC_E_INVALID, "unknown tuning key '%s'", key);
     return GCC_OK;
 }
