@@ -113,6 +113,17 @@ __device__ __forceinline__ u32 in_c(const u32* bm, u32 v) {
 // ~88/us).
 constexpr u32 kRing = 128;  // u64 entries per wave (1 KiB): pending stays < 64 + 64
 
+// One drain round: the wave unites up to 64 ring entries, one per lane. Out of line: it runs rarely, and
+// inlined at each of the hot loop's 8 push sites it multiplied the loop body ~8x (I-cache, registers).
+__device__ __attribute__((noinline)) void ring_drain(const u64* ring, u32 wd, u32 pending, u32* parent) {
+    const u32 lane = threadIdx.x & 63;
+    if (lane < pending) {
+        const u64 e = ring[(wd + lane) & (kRing - 1)];
+        NoCount c;
+        UF::unite(parent, (u32)e, (u32)(e >> 32), c);
+    }
+}
+
 __device__ __forceinline__ void ring_push(bool slow, u32 a, u32 b, u64* ring, u32& wq, u32& wd, u32* parent,
                                           u32 drain_at) {
     const unsigned long long m = __ballot(slow);
@@ -122,11 +133,7 @@ __device__ __forceinline__ void ring_push(bool slow, u32 a, u32 b, u64* ring, u3
     wq += (u32)__popcll(m);
     const u32 pending = wq - wd;
     if (pending >= drain_at) {  // wave-uniform: drain one round (up to 64 edges), one edge per lane
-        if (lane < pending) {
-            const u64 e = ring[(wd + lane) & (kRing - 1)];
-            NoCount c;
-            UF::unite(parent, (u32)e, (u32)(e >> 32), c);
-        }
+        ring_drain(ring, wd, pending, parent);
         wd += pending < 64 ? pending : 64;
     }
 }
