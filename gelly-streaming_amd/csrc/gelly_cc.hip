@@ -645,6 +645,7 @@ struct FoldTune {
     bool pipe = true;  // software-pipelined filtered stream (next round's loads in flight during filtering)
     u32 drain_at = 64;  // a wave drains its slow-edge ring once this many edges are pending (1..64)
     bool seed_nt = true;  // non-temporal loads in the BFS passes (false: the prefix may stay in the MALL)
+    bool seed_global = false;  // also seed when the bitmap does not fit LDS (global-bitmap BFS lookups)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -942,7 +943,10 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
     }
     int rc = GCC_OK;
     u64 b = 0;
-    const bool seeded = h->pending_reset && h->filter_enabled() && t.seed && n >= t.filter_min_batch &&
+    // seeding pays when the BFS lookups are LDS-resident; beyond that (C4: 8 MiB bitmap) the sampled start
+    // measured faster (profiles/r1_sweep_c4_seed.log)
+    const bool seed_fits = (u64)h->nwords() + (h->nwords() & 1) <= kLdsBitmapMaxWords || t.seed_global;
+    const bool seeded = h->pending_reset && h->filter_enabled() && t.seed && seed_fits && n >= t.filter_min_batch &&
                         ((reinterpret_cast<uintptr_t>(h->d_parent) | reinterpret_cast<uintptr_t>(h->d_spare)) & 15) == 0;
     double refresh[3] = {t.refresh[0], t.refresh[1], t.refresh[2]};
     if (seeded) {
@@ -1486,6 +1490,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "pipe") t.pipe = value != 0;
     else if (k == "drain_at") t.drain_at = (u32)std::max(1.0, std::min(64.0, value));
     else if (k == "seed_nt") t.seed_nt = value != 0;
+    else if (k == "seed_global") t.seed_global = value != 0;
     else if (k == "seed_passes") t.seed_passes = std::max(0, std::min(16, (int)value));
     else if (k == "seed_div") t.seed_div = std::max<u64>(1, (u64)value);
     else if (k == "seed_refresh") t.seed_refresh = value;
