@@ -102,12 +102,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if os.environ.get("GELLY_SHARE_GPU"):  # rehearsal: every rank on cuda:0 (never for a measurement)
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        backend = os.environ.get("GELLY_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI; gloo: 1-GPU rehearsal
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
 
     from gelly_stream import generators as G
     from gelly_stream.distributed import ForestGroup, TorchDisjointSet
@@ -128,6 +134,7 @@ def main():
 
     fold_events = []
     host_fold_s = []
+    merge_events = []  # (after fold, after merge) on the forest's stream, N > 1
 
     def step(timed):
         forest.ds.reset()
@@ -144,6 +151,10 @@ def main():
                 fold_events.append((ev0, ev1, e - b))
             if group is not None:
                 group.merge_forest(forest)
+                if timed:
+                    ev2 = torch.cuda.Event(enable_timing=True)
+                    ev2.record(stream)
+                    merge_events.append((ev1, ev2))
             else:
                 forest.compress()
 
@@ -196,6 +207,7 @@ def main():
     if prof and dominant in prof.get("kernel", "") and abs(prof.get("edges_per_launch", 0) - dom_edges) <= 0.01 * dom_edges:
         traffic = prof["hbm_bytes_per_launch"]
 
+    merge_ms = [a.elapsed_time(b) for a, b in merge_events]
     labels = forest.ds.labels()
     seen = int(np.count_nonzero(labels != 0xFFFFFFFF))
     comps = int(np.count_nonzero(labels == np.arange(V, dtype=np.uint32)))
@@ -231,7 +243,8 @@ def main():
             "windows_per_step": n_windows,
             "window_edges": W,
             "parallelism": f"dp{world}",
-            "merge": "butterfly p2p over RCCL" if world > 1 else "none",
+            "merge": ("compact all_gather over RCCL (giant bitmap + others list; label butterfly fallback)"
+                      if world > 1 else "none"),
         },
         "roofline": {
             "bound": "hbm",
@@ -253,6 +266,8 @@ def main():
                          "host_enqueue_ms_avg": sum(host_fold_s) / len(host_fold_s) * 1e3},
         },
         "summary": {"seen": seen, "components": comps},
+        "merge": ({"ms_avg": sum(merge_ms) / len(merge_ms), "last": group.last} if group is not None and merge_ms
+                  else None),
     }
     if world == 1 and args.cpu_seconds > 0:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)

@@ -576,6 +576,165 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(u32* __restrict__ par
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Cross-GPU merge message (include/gelly_cc.h: header, giant bitmap, (v, label) list of the other seen ids).
+// ------------------------------------------------------------------------------------------------
+constexpr unsigned kMsgWordsPerBlock = 64;  // 4096 ids per block; one atomicAdd per block with "others"
+
+// Encode from canonical labels. Each block owns kMsgWordsPerBlock consecutive 64-id words: pass 1 counts its
+// "others" (4 words in flight per wave), one atomicAdd reserves its slice of the list, pass 2 writes the bitmap
+// words and the pairs (the block's 16 KiB of labels are re-read from L2). msg_header_kernel runs first.
+__global__ __launch_bounds__(kBlock) void msg_encode_kernel(const u32* __restrict__ labels, u32 n, u32* __restrict__ hdr,
+                                                            u64* __restrict__ bits, u32* __restrict__ others, u64 cap) {
+    __shared__ u32 s_cnt[kBlock / 64];
+    __shared__ u32 s_base;
+    constexpr int kW = kMsgWordsPerBlock / (kBlock / 64);  // words per wave
+    const u32 g = hdr[0];
+    const u64 nw = ((u64)n + 63) / 64;
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const u64 w0 = (u64)blockIdx.x * kMsgWordsPerBlock + (u64)wave * kW;
+    u32 l[kW];
+#pragma unroll
+    for (int k = 0; k < kW; ++k) {
+        const u64 v = (w0 + k) * 64 + lane;
+        l[k] = (w0 + k < nw && v < n) ? labels[v] : UNSEEN;
+    }
+    u32 cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kW; ++k) cnt += (u32)__popcll(__ballot(l[k] != UNSEEN && l[k] != g));
+    if (lane == 0) s_cnt[wave] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u32 tot = 0;
+        for (int k = 0; k < kBlock / 64; ++k) {
+            const u32 c = s_cnt[k];
+            s_cnt[k] = tot;  // exclusive prefix over the block's waves
+            tot += c;
+        }
+        s_base = tot ? atomicAdd(&hdr[1], tot) : 0;  // hdr[1] ends as the true count
+    }
+    __syncthreads();
+    u64 pos = (u64)s_base + s_cnt[wave];
+#pragma unroll
+    for (int k = 0; k < kW; ++k) {
+        const u64 w = w0 + k;
+        const unsigned long long in_g = __ballot(l[k] != UNSEEN && l[k] == g);
+        const unsigned long long oth = __ballot(l[k] != UNSEEN && l[k] != g);
+        if (lane == 0 && w < nw) bits[w] = in_g;
+        if ((oth >> lane) & 1ull) {
+            const u64 q = pos + (u64)__popcll(oth & ((1ull << lane) - 1ull));
+            if (q < cap) {
+                others[2 * q] = (u32)(w * 64 + lane);
+                others[2 * q + 1] = l[k];
+            }
+        }
+        pos += (u64)__popcll(oth);
+    }
+}
+
+__global__ void msg_header_kernel(u32* __restrict__ hdr, const u32* __restrict__ giant_root, u32 has_giant, u32 n) {
+    hdr[0] = has_giant ? *giant_root : UNSEEN;
+    hdr[1] = 0;
+    hdr[2] = n;
+    hdr[3] = 0;
+}
+
+// Absorbing the P-1 peer messages of an all_gather (gcc_forest_absorb_many), two launches:
+//  msg_overlap_kernel: for each peer p, does its giant G_p share an id with this forest's tracked component T
+//    (bitmap `mine`, root R; valid forever since components only grow)? If so, witness[p] = one shared id.
+//  msg_absorb_kernel: for the overlapping peers, unite(witness_p, g_p) joins G_p's root to T (block 0), after
+//    which every id of G_p is connected to R — so the union U of their bitmaps only needs its ids OUTSIDE T
+//    united with R, each ONCE however many peers hold it (one 64-id word per wave, one id per lane). Peers
+//    without overlap (or no T at all) are absorbed id by id against their own root. Then the (v, label) lists.
+constexpr u32 kMaxPeers = 64;
+
+__global__ __launch_bounds__(kBlock) void msg_overlap_kernel(const char* __restrict__ msgs, u64 stride, u32 count,
+                                                             u32 skip, u32 n, const u64* __restrict__ mine,
+                                                             u32* __restrict__ witness) {
+    const u64 nw = ((u64)n + 63) / 64;
+    const u64 chunks = (nw + 63) / 64;  // one word per lane
+    const u32 lane = threadIdx.x & 63;
+    const u64 wave = (u64)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const u64 waves = (u64)gridDim.x * (kBlock / 64);
+    for (u64 t = wave; t < (u64)count * chunks; t += waves) {
+        const u32 p = (u32)(t / chunks);
+        if (p == skip) continue;
+        const u32* hdr = reinterpret_cast<const u32*>(msgs + p * stride);
+        if (hdr[2] != n || hdr[0] >= n) continue;
+        if (__hip_atomic_load(&witness[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != UNSEEN) continue;
+        const u64 w = (t - (u64)p * chunks) * 64 + lane;
+        u64 both = 0;
+        if (w < nw) both = reinterpret_cast<const u64*>(msgs + p * stride + GCC_MSG_HEADER_BYTES)[w] & mine[w];
+        const unsigned long long wb = __ballot(both != 0);
+        if (wb && lane == (u32)__builtin_ctzll(wb)) witness[p] = (u32)(w * 64 + __builtin_ctzll(both));  // any one
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ parent, const char* __restrict__ msgs,
+                                                            u64 stride, u32 count, u32 skip, u64 cap, u32 n,
+                                                            const u64* __restrict__ mine, const u32* __restrict__ tracked,
+                                                            const u32* __restrict__ witness) {
+    __shared__ u32 s_g[kMaxPeers];
+    __shared__ u32 s_w[kMaxPeers];
+    NoCount c;
+    const u32 lane = threadIdx.x & 63;
+    if (threadIdx.x < kMaxPeers) {
+        u32 g = UNSEEN, wv = UNSEEN;
+        if (threadIdx.x < count && threadIdx.x != skip) {
+            const u32* hdr = reinterpret_cast<const u32*>(msgs + threadIdx.x * stride);
+            if (hdr[2] == n && hdr[0] < n) {
+                g = hdr[0];
+                wv = mine ? witness[threadIdx.x] : UNSEEN;
+            }
+        }
+        s_g[threadIdx.x] = g;
+        s_w[threadIdx.x] = wv;
+        if (blockIdx.x == 0 && wv != UNSEEN && wv != g) UF::unite(parent, wv, g, c);  // G_p joins T
+    }
+    __syncthreads();
+    const u32 R = mine ? *tracked : UNSEEN;
+    const u64 nw = ((u64)n + 63) / 64;
+    const u64 wave = (u64)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const u64 waves = (u64)gridDim.x * (kBlock / 64);
+    for (u64 w = wave; w < nw; w += waves) {
+        // lane p < count loads peer p's word; the overlapping peers' words are OR-ed across the wave
+        u64 m = 0, lone = 0;
+        if (lane < count && s_g[lane] != UNSEEN) {
+            m = reinterpret_cast<const u64*>(msgs + lane * stride + GCC_MSG_HEADER_BYTES)[w];
+            if (s_w[lane] == UNSEEN) {
+                lone = m;  // no overlap with T: absorbed against its own root below
+                m = 0;
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off, 64);
+        const u64 v = w * 64 + lane;
+        if (m) {
+            const u64 todo = m & ~mine[w];
+            if (((todo >> lane) & 1ull) && (u32)v != R) UF::unite(parent, (u32)v, R, c);
+        }
+        unsigned long long lb = __ballot(lone != 0);
+        while (lb) {  // rare: peers whose giant does not touch T (or no T)
+            const u32 p = (u32)__builtin_ctzll(lb);
+            lb &= lb - 1;
+            const u64 mp = __shfl(lone, (int)p, 64);
+            if (((mp >> lane) & 1ull) && (u32)v != s_g[p]) UF::unite(parent, (u32)v, s_g[p], c);
+        }
+    }
+    const u64 stride_t = (u64)gridDim.x * kBlock;
+    const u64 tid = (u64)blockIdx.x * kBlock + threadIdx.x;
+    for (u32 p = 0; p < count; ++p) {
+        if (p == skip) continue;
+        const u32* hdr = reinterpret_cast<const u32*>(msgs + p * stride);
+        if (hdr[2] != n) continue;
+        const u32* others = reinterpret_cast<const u32*>(msgs + p * stride + GCC_MSG_HEADER_BYTES + nw * sizeof(u64));
+        const u64 cnt = min((u64)hdr[1], cap);
+        for (u64 k = tid; k < cnt; k += stride_t) {
+            const u32 v = others[2 * k], l = others[2 * k + 1];
+            if (v < n && l < n) UF::unite(parent, v, l, c);
+        }
+    }
+}
+
 // counts[0] += #seen, counts[1] += #roots (= #components)
 __global__ __launch_bounds__(kBlock) void count_kernel(const u32* __restrict__ parent, u32 n,
                                                        unsigned long long* __restrict__ counts) {
@@ -682,6 +841,7 @@ struct gcc_forest {
 
     // scratch for cross-device merges
     u32* d_scratch = nullptr;
+    u32* d_witness = nullptr;  // absorb_many: per-peer id shared with the tracked component
 
     unsigned long long* d_counts = nullptr;
 
@@ -1189,6 +1349,7 @@ int gcc_forest_destroy(gcc_forest* h) {
         if (h->d_spare) (void)hipFree(h->d_spare);
     }
     if (h->d_scratch) (void)hipFree(h->d_scratch);
+    if (h->d_witness) (void)hipFree(h->d_witness);
     if (h->d_bits) (void)hipFree(h->d_bits);
     if (h->d_giant) (void)hipFree(h->d_giant);
     if (h->d_qcount) (void)hipFree(h->d_qcount);
@@ -1397,6 +1558,61 @@ int gcc_forest_merge(gcc_forest* into, gcc_forest* from) {
     }
     HIP_TRY(hipEventDestroy(ev));
     return rc;
+}
+
+uint64_t gcc_msg_bytes(uint32_t id_capacity, uint64_t cap_others) {
+    return GCC_MSG_HEADER_BYTES + (((u64)id_capacity + 63) / 64) * sizeof(u64) + cap_others * 2 * sizeof(u32);
+}
+
+int gcc_forest_encode(gcc_forest* h, void* d_msg, uint64_t cap_others) {
+    CHECK_ARG(h && d_msg, "null argument");
+    CHECK_ARG((reinterpret_cast<uintptr_t>(d_msg) & 15) == 0, "message buffer must be 16-byte aligned");
+    DeviceGuard g(h->device);
+    int rc = compress_async(h);
+    if (rc) return rc;
+    u32* hdr = reinterpret_cast<u32*>(d_msg);
+    u64* bits = reinterpret_cast<u64*>(static_cast<char*>(d_msg) + GCC_MSG_HEADER_BYTES);
+    u32* others = reinterpret_cast<u32*>(bits + ((u64)h->cap + 63) / 64);
+    hipLaunchKernelGGL(msg_header_kernel, dim3(1), dim3(1), 0, h->stream, hdr,
+                       h->d_giant ? h->d_giant + h->giant_slot : hdr, h->has_giant ? 1u : 0u, h->cap);
+    const u64 nw = ((u64)h->cap + 63) / 64;
+    hipLaunchKernelGGL(msg_encode_kernel, dim3((unsigned)((nw + kMsgWordsPerBlock - 1) / kMsgWordsPerBlock)), dim3(kBlock),
+                       0, h->stream, h->d_parent, h->cap, hdr, bits, others, (u64)cap_others);
+    HIP_TRY(hipGetLastError());
+    return GCC_OK;
+}
+
+int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_bytes, uint32_t count, uint32_t skip,
+                           uint64_t cap_others) {
+    CHECK_ARG(h && (d_msgs || count == 0), "null argument");
+    CHECK_ARG(((reinterpret_cast<uintptr_t>(d_msgs) | stride_bytes) & 15) == 0, "messages must be 16-byte aligned");
+    CHECK_ARG(count <= 1 || stride_bytes >= gcc_msg_bytes(h->cap, cap_others), "stride smaller than a message");
+    CHECK_ARG(count <= kMaxPeers, "at most 64 messages per call");
+    DeviceGuard g(h->device);
+    int rc = flush(h);
+    if (rc) return rc;
+    if (count == 0 || (count == 1 && skip == 0)) return GCC_OK;
+    const u64 nw = ((u64)h->cap + 63) / 64;
+    const bool tracked = h->has_giant && h->d_bits;
+    const u64* mine = tracked ? h->d_bits : nullptr;
+    const char* msgs = static_cast<const char*>(d_msgs);
+    if (tracked) {
+        if (!h->d_witness) HIP_TRY(hipMalloc((void**)&h->d_witness, kMaxPeers * sizeof(u32)));
+        HIP_TRY(hipMemsetAsync(h->d_witness, 0xFF, kMaxPeers * sizeof(u32), h->stream));
+        hipLaunchKernelGGL(msg_overlap_kernel, dim3(grid_for((u64)count * ((nw + 63) / 64) * 64, kMaxGrid)), dim3(kBlock),
+                           0, h->stream, msgs, (u64)stride_bytes, count, skip, h->cap, mine, h->d_witness);
+    }
+    const u64 work = std::max<u64>(nw * 64, cap_others);  // one word per wave; one list entry per lane
+    hipLaunchKernelGGL(msg_absorb_kernel, dim3(grid_for(work, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent, msgs,
+                       (u64)stride_bytes, count, skip, (u64)cap_others, h->cap, mine,
+                       tracked ? h->d_giant + h->giant_slot : nullptr, tracked ? h->d_witness : nullptr);
+    HIP_TRY(hipGetLastError());
+    mark_mutated(h);
+    return GCC_OK;
+}
+
+int gcc_forest_absorb(gcc_forest* h, const void* d_msg, uint64_t cap_others) {
+    return gcc_forest_absorb_many(h, d_msg, 0, 1, UINT32_MAX, cap_others);
 }
 
 int gcc_forest_compress(gcc_forest* h) {

@@ -6,11 +6,14 @@ parallelism-1 ``Merger`` (…/SummaryAggregation.java:107-119). SummaryTreeReduc
 pairs partitions up in a log2 tree instead.
 
 MI355X form: every rank (one process per GPU) keeps a full-range forest. At a window boundary each rank
-compresses its forest to canonical min-id labels and runs a butterfly over torch.distributed point-to-point
-(RCCL over xGMI; gloo in the CPU tests): in round r it swaps its label array with rank ^ 2^r and unions the
-partner's (v, label[v]) pairs into its own forest. After log2(P) rounds every rank holds the global partition
-— exactly the forest the reference's reduce + Merger emit — and no rank is a serial bottleneck. Each round
-moves V * 4 bytes over one direct xGMI link. A non-power-of-two world falls back to all_gather + union.
+compresses its forest to canonical min-id labels and encodes it as a compact message (include/gelly_cc.h:
+header, bitmap of the largest component, (v, label) list of the other seen ids — 1/32 of the label array
+when one component dominates). One RCCL all_gather over xGMI moves every rank's message to every rank
+(the list capacity is speculative — the last window's need x1.5 — and the gathered headers say whether a
+repair round is needed), and each rank absorbs the P-1 partitions into its own forest. Every rank ends with the global partition — exactly the forest the reference's reduce +
+Merger emit — in one collective, with no serial bottleneck. When the compact form is not smaller than the
+label array (no dominant component), the labels themselves are exchanged: a butterfly of log2(P) rounds of
+RCCL send/recv with rank ^ 2^r for a power-of-two world, all_gather otherwise.
 """
 from __future__ import annotations
 
@@ -18,11 +21,17 @@ from typing import Optional, Protocol
 
 
 class ExchangeForest(Protocol):
-    """What the butterfly needs from a forest."""
+    """What the merge needs from a forest."""
+
+    id_capacity: int
 
     def compress(self) -> None: ...                     # canonicalise (async on the comm stream)
     def exchange_tensor(self): ...                      # torch tensor holding the labels (same device as comms)
     def absorb(self, labels) -> None: ...               # forest := forest ∪ {(v, labels[v])}
+    def new_bytes(self, n: int): ...                    # uint8 tensor of n bytes on the comm device
+    def encode(self, msg, cap_others: int) -> None: ... # compress + write the message into msg
+    def absorb_msg(self, msg, cap_others: int) -> None: ...  # forest := forest ∪ the message's partition
+    def absorb_msgs(self, msgs, stride: int, count: int, skip: int, cap_others: int) -> None: ...  # all but `skip`
 
 
 class TorchDisjointSet:
@@ -52,22 +61,51 @@ class TorchDisjointSet:
     def absorb(self, labels) -> None:
         self.ds.merge_labels_device(labels.data_ptr(), labels.numel())
 
+    def new_bytes(self, n: int):
+        import torch
+
+        return torch.empty(int(n), dtype=torch.uint8, device=f"cuda:{self.device}")
+
+    def encode(self, msg, cap_others: int) -> None:
+        self.ds.encode_message(msg.data_ptr(), cap_others)
+
+    def absorb_msg(self, msg, cap_others: int) -> None:
+        self.ds.absorb_message(msg.data_ptr(), cap_others)
+
+    def absorb_msgs(self, msgs, stride: int, count: int, skip: int, cap_others: int) -> None:
+        self.ds.absorb_messages(msgs.data_ptr(), stride, count, skip, cap_others)
+
     def __getattr__(self, name):  # delegate the DisjointSet surface (find, getMatches, fold_device, ...)
         return getattr(self.ds, name)
 
 
-class ForestGroup:
-    """Butterfly min-label merge of one forest per rank."""
+def _round16(n: int) -> int:
+    return (int(n) + 15) // 16 * 16
 
-    def __init__(self, group=None):
+
+class ForestGroup:
+    """Cross-rank merge of one forest per rank (mode "auto": compact all_gather, label exchange fallback;
+    "labels": always exchange label arrays)."""
+
+    def __init__(self, group=None, mode: str = "auto"):
         import torch.distributed as dist
 
+        if mode not in ("auto", "labels"):
+            raise ValueError(f"unknown merge mode {mode!r}")
         self._dist = dist
         self.group = group
+        self.mode = mode
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self._recv = None
         self._gather = None
+        self._cap = 0          # list capacity of the message buffer (grows, never shrinks)
+        self._msg = None
+        self._recv_msg = None
+        self._hdr_host = None
+        self._hdr_event = None
+        self._prefer_labels = False  # the compact form did not pay: exchange labels from now on
+        self.last = {}         # what the last merge sent (measurement / tests)
 
     def _global(self, r: int) -> int:
         return r if self.group is None else self._dist.get_global_rank(self.group, r)
@@ -77,12 +115,91 @@ class ForestGroup:
             self._recv = t.new_empty(t.shape)
         return self._recv
 
+    def _all_gather_flat(self, out, inp) -> None:
+        """out (world * inp.numel()) := concatenation of every rank's inp (RCCL: one allgather)."""
+        try:
+            self._dist.all_gather_into_tensor(out, inp, group=self.group)
+        except (RuntimeError, AttributeError, NotImplementedError):  # backends without the flat form (gloo)
+            n = inp.numel()
+            self._dist.all_gather([out[r * n:(r + 1) * n] for r in range(self.world)], inp, group=self.group)
+
     def merge_forest(self, forest: ExchangeForest) -> None:
         """forest := union of every rank's forest (collective: every rank must call it)."""
-        dist = self._dist
         forest.compress()
         if self.world == 1:
             return
+        if self.mode == "auto" and self._merge_compact(forest):
+            return
+        self._merge_labels(forest)
+        self.last = {"compact": False, "rounds": 1, "full_bytes": 4 * int(forest.id_capacity)}
+
+    def _merge_compact(self, forest: ExchangeForest) -> bool:
+        """One all_gather of messages at a speculative list capacity; absorb + compress are enqueued before the
+        host looks at the gathered headers. If some rank's list did not fit, the (exact, since union is
+        idempotent) exchange is repeated with a larger capacity; if the compact form stops paying, the label
+        exchange finishes the merge and later merges go straight to it."""
+        from .native import MSG_HEADER_BYTES, msg_bytes
+
+        if self._prefer_labels:
+            return False
+        V = int(forest.id_capacity)
+        full = 4 * V
+        if self._cap == 0:
+            self._cap = max(1024, V // 64)
+        rounds = 0
+        while True:
+            cap = self._cap
+            size = _round16(msg_bytes(V, cap))
+            if size >= full:
+                self._prefer_labels = True
+                if rounds == 0:
+                    return False
+                self._merge_labels(forest)  # finish exactly (the forest already holds a partial union)
+                self.last.update(compact=False, rounds=rounds + 1)
+                return True
+            if self._msg is None or self._msg.numel() < size:
+                self._msg = forest.new_bytes(size)
+            if self._recv_msg is None or self._recv_msg.numel() < self.world * size:
+                self._recv_msg = forest.new_bytes(self.world * size)
+            forest.encode(self._msg, cap)
+            recv = self._recv_msg[:self.world * size]
+            self._all_gather_flat(recv, self._msg[:size])
+            hdrs = self._copy_headers(recv.view(self.world, size)[:, :MSG_HEADER_BYTES])
+            forest.absorb_msgs(recv, size, self.world, self.rank, cap)
+            forest.compress()
+            counts = self._wait_headers(hdrs)[:, 1]
+            nmax = int(counts.max())
+            rounds += 1
+            self.last = {"n_others": [int(c) for c in counts], "cap": cap, "bytes": size, "full_bytes": full,
+                         "compact": True, "rounds": rounds}
+            if nmax <= cap:
+                if 4 * nmax < cap and cap > 1024:  # shrink slowly toward 1.5x the observed need
+                    self._cap = max(1024, 3 * nmax // 2, cap // 2)
+                return True
+            self._cap = max(3 * nmax // 2, 2 * cap)
+
+    def _copy_headers(self, hdr_view):
+        """Start the device->host copy of the gathered headers (pinned, async) and return a handle."""
+        import torch
+
+        h = hdr_view.contiguous()
+        if h.device.type == "cpu":
+            return h.clone()
+        if self._hdr_host is None or self._hdr_host.shape != h.shape:
+            self._hdr_host = torch.empty(h.shape, dtype=h.dtype, pin_memory=True)
+        self._hdr_host.copy_(h, non_blocking=True)
+        self._hdr_event = torch.cuda.Event()
+        self._hdr_event.record()
+        return self._hdr_host
+
+    def _wait_headers(self, h):
+        if self._hdr_event is not None:
+            self._hdr_event.synchronize()
+            self._hdr_event = None
+        return h.numpy().view("<u4").reshape(self.world, 4)
+
+    def _merge_labels(self, forest: ExchangeForest) -> None:
+        dist = self._dist
         buf = forest.exchange_tensor()
         if self.world & (self.world - 1) == 0:
             recv = self._recv_like(buf)

@@ -85,7 +85,18 @@ _SIGS = {
     "gcc_forest_last_fold_ms": (c_int, [c_void_p, POINTER(c_float)]),
     "gcc_forest_fold_profile": (c_int, [c_void_p, c_char_p, c_uint64]),
     "gcc_forest_tune": (c_int, [c_void_p, c_char_p, ctypes.c_double]),
+    "gcc_msg_bytes": (c_uint64, [c_uint32, c_uint64]),
+    "gcc_forest_encode": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_forest_absorb": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_forest_absorb_many": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_uint64]),
 }
+
+MSG_HEADER_BYTES = 16  # GCC_MSG_HEADER_BYTES
+
+
+def msg_bytes(id_capacity: int, cap_others: int) -> int:
+    """gcc_msg_bytes: size of a cross-GPU merge message (header + giant bitmap + cap_others (v, label) pairs)."""
+    return MSG_HEADER_BYTES + (int(id_capacity) + 63) // 64 * 8 + int(cap_others) * 8
 
 _lib = None
 

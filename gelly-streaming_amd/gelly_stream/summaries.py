@@ -178,6 +178,21 @@ class DisjointSet:
         call("gcc_forest_merge_labels_device", self.handle, c_void_p(d_labels), int(n))
         self._dirty()
 
+    def encode_message(self, d_msg: int, cap_others: int) -> None:
+        """Compress, then write the cross-GPU merge message (include/gelly_cc.h layout) into d_msg (async)."""
+        call("gcc_forest_encode", self.handle, c_void_p(d_msg), int(cap_others))
+
+    def absorb_message(self, d_msg: int, cap_others: int) -> None:
+        """self := self ∪ the partition of a message written with the same id_capacity and cap_others."""
+        call("gcc_forest_absorb", self.handle, c_void_p(d_msg), int(cap_others))
+        self._dirty()
+
+    def absorb_messages(self, d_msgs: int, stride: int, count: int, skip: int, cap_others: int) -> None:
+        """Absorb `count` messages laid out every `stride` bytes from d_msgs, except number `skip` (one launch)."""
+        call("gcc_forest_absorb_many", self.handle, c_void_p(d_msgs), int(stride), int(count), int(skip) & 0xFFFFFFFF,
+             int(cap_others))
+        self._dirty()
+
     def compress(self) -> None:
         """Canonicalise (async): afterwards device_ptr() holds the min-id labels."""
         call("gcc_forest_compress", self.handle)

@@ -111,6 +111,26 @@ int gcc_forest_merge(gcc_forest* into, gcc_forest* from); /* into := into ∪ fr
  * ordered on into's stream (the receive side of the cross-GPU merge) */
 int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, uint32_t n);
 
+/* ---- cross-GPU merge message: the partial forest as the RCCL payload (replaces the Kryo-serialised
+ * DisjointSet that SummaryBulkAggregation.java:81-83 ships to the one task running timeWindowAll.reduce).
+ * Layout (one device buffer, gcc_msg_bytes(id_capacity, cap_others) bytes):
+ *   u32 header[4] = { g, n_others, id_capacity, 0 }
+ *   u64 bits[ceil(id_capacity / 64)]      bit v set <=> label[v] == g   (g = the tracked giant's root)
+ *   u32 others[2 * cap_others]            (v, label[v]) for every other seen v (n_others of them, any order)
+ * The partition it encodes is exactly the forest's: {(v, g) : bit v} ∪ {(v, label[v]) : others}. */
+#define GCC_MSG_HEADER_BYTES 16
+uint64_t gcc_msg_bytes(uint32_t id_capacity, uint64_t cap_others);
+/* compress, then write the message into d_msg (async on h's stream); the header's n_others is the true
+ * count even when it exceeds cap_others (then only cap_others entries are written: re-encode larger) */
+int gcc_forest_encode(gcc_forest* h, void* d_msg, uint64_t cap_others);
+/* h := h ∪ the message's partition (async); cap_others = the layout the message was written with, and its
+ * n_others must not exceed it. The sender must have the same id_capacity (else the message is ignored). */
+int gcc_forest_absorb(gcc_forest* h, const void* d_msg, uint64_t cap_others);
+/* the same for `count` messages at d_msgs + i * stride_bytes (i != skip: this rank's own), in one launch —
+ * the receive side of the all_gather; stride_bytes >= gcc_msg_bytes(id_capacity, cap_others), 16-B aligned */
+int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_bytes, uint32_t count, uint32_t skip,
+                           uint64_t cap_others);
+
 /* ---- summary reads (DisjointSet.find :71-85, getMatches :49-51; the emitted summary per window) ---- */
 int gcc_forest_compress(gcc_forest* h); /* async: canonical labels; afterwards gcc_forest_device_ptr = labels */
 int gcc_forest_labels(gcc_forest* h, uint32_t* out, uint32_t n); /* compress + copy n labels to host */

@@ -324,3 +324,74 @@ def test_fold_timing_events():
     ds.enable_timing(1)
     ds.fold(G.generate_host(cfg))
     assert ds.last_fold_ms() > 0.0
+
+
+# ---- cross-GPU merge message (include/gelly_cc.h): encode / absorb, the RCCL payload's two ends ----
+def encode(torch_cuda, ds, cap):
+    msg = torch_cuda.zeros(native.msg_bytes(ds.id_capacity, cap) + 16, dtype=torch_cuda.uint8, device="cuda:0")
+    ds.encode_message(msg.data_ptr(), cap)
+    torch_cuda.cuda.synchronize()
+    hdr = msg[:16].cpu().numpy().view("<u4")
+    return msg, hdr
+
+
+def test_merge_message_ranks_on_one_gpu(torch_cuda):
+    """P forests on one GPU play the ranks of ForestGroup's compact all_gather: per window each folds its chunk,
+    encodes, absorbs the P-1 other messages, and must hold the global partition (oracle) — every window."""
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=16, n_edges=1 << 20)
+    E, V = cfg.info()
+    starts = np.asarray([0, 1000, 1 << 17, 1 << 19, E], dtype=np.uint64)
+    want = orc.cc_stream(G.generate_host(cfg), starts, V, partitions=4, threads=4, want_labels=True)["labels"]
+    d = device_stream(torch_cuda, cfg)
+    P, cap = 4, V
+    ranks = [DisjointSet(V) for _ in range(P)]
+    for w in range(len(starts) - 1):
+        b, e = int(starts[w]), int(starts[w + 1])
+        msgs = []
+        for r, ds in enumerate(ranks):
+            lo, hi = b + (e - b) * r // P, b + (e - b) * (r + 1) // P
+            ds.fold_device(d.data_ptr() + 8 * lo, hi - lo)
+            msg, hdr = encode(torch_cuda, ds, cap)
+            lab = ds.labels()
+            seen = lab != UNSEEN
+            assert hdr[2] == V
+            assert hdr[1] == int(np.count_nonzero(seen & (lab != hdr[0]))), (w, r)
+            msgs.append(msg)
+        stride = msgs[0].numel()
+        packed = torch_cuda.cat(msgs)  # the all_gather receive buffer: rank p's message at p * stride
+        for r, ds in enumerate(ranks):
+            if r % 2:  # one fused launch over all peers (the ForestGroup path)
+                ds.absorb_messages(packed.data_ptr(), stride, P, r, cap)
+            else:
+                for p, msg in enumerate(msgs):
+                    if p != r:
+                        ds.absorb_message(msg.data_ptr(), cap)
+        for r, ds in enumerate(ranks):
+            assert first_mismatch(ds.labels(), want[w]) is None, (w, r, first_mismatch(ds.labels(), want[w]))
+    for ds in ranks:
+        ds.close()
+
+
+def test_merge_message_full_c2_round_trip(torch_cuda):
+    """Full C2 forest -> message -> empty forest: the same partition; the message is ~1/32 of the labels."""
+    cfg = G.CONFIGS["c2_rmat20"]
+    E, V = cfg.info()
+    d = device_stream(torch_cuda, cfg)
+    a = DisjointSet(V)
+    a.fold_device(d.data_ptr(), E)
+    la = a.labels().copy()
+    msg, hdr = encode(torch_cuda, a, cap=1)  # list too small: the header still reports the true count
+    n_oth = int(hdr[1])
+    assert n_oth == int(np.count_nonzero((la != UNSEEN) & (la != hdr[0])))
+    assert native.msg_bytes(V, n_oth) < 4 * V // 8
+    msg, hdr = encode(torch_cuda, a, cap=n_oth)
+    b = DisjointSet(V)
+    b.absorb_message(msg.data_ptr(), n_oth)
+    assert np.array_equal(b.labels(), la)
+    # absorbing into a forest that already holds part of the partition: still the union
+    c = DisjointSet(V)
+    c.fold_device(d.data_ptr(), E // 5)
+    c.absorb_message(msg.data_ptr(), n_oth)
+    assert np.array_equal(c.labels(), la)
+    for x in (a, b, c):
+        x.close()
