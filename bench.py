@@ -23,7 +23,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gelly-streaming_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, Chip-level parameters)
-BYTES_PER_EDGE = 16  # algorithmic: 8 B edge stream + 2 x 4 B parent reads
+BYTES_PER_EDGE = 16  # algorithmic, whole fold: 8 B edge stream + 2 x 4 B parent reads
+# per-kernel algorithmic bytes: (bytes, per "edge" of the launch | per "id" of the forest)
+KERNEL_BYTES = {
+    "fold_filtered_kernel": (8, "edge"),    # the edge stream (skipped edges need no parent access)
+    "seed_bfs_kernel": (8, "edge"),         # the prefix edge stream (bitmap in LDS)
+    "fold_kernel": (16, "edge"),            # edge + both parents
+    "compress_bits_kernel": (8.125, "id"),  # parent read + label write + 1 bitmap bit
+    "seed_pack_kernel": (5.125, "id"),      # flag byte read + parent write + 1 bitmap bit (the init variant)
+    "seed_hub_kernel": (1.125, "id"),       # flag byte + bitmap bit cleared
+}
 
 
 def parse():
@@ -36,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = min(16, cores))")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--phase-timing", choices=["timed", "after", "off"], default="after",
+                    help="per-kernel dispatch events in the timed steps, in extra steps after them, or not at all")
     return ap.parse_args()
 
 
@@ -132,26 +143,23 @@ def main():
     group = ForestGroup() if world > 1 else None
     base_ptr = d_edges.data_ptr()
 
-    fold_events = []
     host_fold_s = []
-    merge_events = []  # (after fold, after merge) on the forest's stream, N > 1
+    merge_events = []  # (before merge, after merge) on the forest's stream, N > 1, instrumented steps only
 
-    def step(timed):
+    def step(instrument):
         forest.ds.reset()
         for w in range(n_windows):
             b, e = starts[w], starts[w + 1]
-            if timed:
-                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                ev0.record(stream)
             th = time.perf_counter()
             forest.ds.fold_device(base_ptr + 8 * b, e - b)
-            if timed:
+            if instrument:
                 host_fold_s.append(time.perf_counter() - th)
-                ev1.record(stream)
-                fold_events.append((ev0, ev1, e - b))
             if group is not None:
+                if instrument:
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev1.record(stream)
                 group.merge_forest(forest)
-                if timed:
+                if instrument:
                     ev2 = torch.cuda.Event(enable_timing=True)
                     ev2.record(stream)
                     merge_events.append((ev1, ev2))
@@ -160,15 +168,18 @@ def main():
 
     for _ in range(args.warmup):
         step(False)
-    forest.ds.enable_timing(1)  # per-phase HIP events on the forest's stream (recorded without syncs)
-    forest.ds.fold_profile()    # drain the warmup log
+    # "timed": every kernel of the timed steps carries its own dispatch start/stop events (hipExtLaunchKernel, no
+    # extra packets); "after": the timed steps run bare and min(steps, 10) instrumented steps follow them
+    timed_inst = args.phase_timing == "timed"
+    forest.ds.enable_timing(1 if timed_inst else 0)
+    forest.ds.fold_profile()  # drain the warmup log
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        step(timed_inst)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -178,33 +189,58 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    inst_steps = args.steps if timed_inst else 0
+    if args.phase_timing == "after":
+        inst_steps = min(args.steps, 10)
+        forest.ds.enable_timing(1)
+        for _ in range(inst_steps):
+            step(True)
+        torch.cuda.synchronize()
+    log = forest.ds.fold_profile()
+    forest.ds.enable_timing(0)
 
-    fold_ms = [a.elapsed_time(b) for a, b, _ in fold_events]
-    fold_edges = [n for _, _, n in fold_events]
-    avg_fold_s = sum(fold_ms) / len(fold_ms) / 1e3
-    avg_fold_edges = sum(fold_edges) / len(fold_edges)
-    pipeline_gbs = BYTES_PER_EDGE * avg_fold_edges / avg_fold_s / 1e9
-
-    # per-phase HIP events of every timed fold (one launch per phase entry), grouped by kernel
-    kernel_of = {"filtered": "fold_filtered_kernel", "sample": "fold_kernel", "plain": "fold_kernel", "seed_hub": "seed_hub_kernel",
-                 "seed_bfs": "seed_bfs_kernel", "seed_init": "seed_init_kernel",
-                 "refresh": "compress_bits_kernel"}
-    phases, kernels = {}, {}
-    for name, ms, n in forest.ds.fold_profile():
-        if name == "begin":
+    # per-kernel durations (each kernel's own dispatch events) and per-fold device spans, grouped by kernel
+    kernel_of = {"filtered": "fold_filtered_kernel", "sample": "fold_kernel", "plain": "fold_kernel",
+                 "seed_hub": "seed_hub_kernel", "seed_bfs": "seed_bfs_kernel", "seed_pack": "seed_pack_kernel",
+                 "seed_init": "seed_pack_kernel", "refresh": "compress_bits_kernel", "compress": "compress_bits_kernel",
+                 "vote": "giant_vote_kernel"}
+    phases, kernels, spans = {}, {}, []
+    for name, ms, n in log:
+        if name == "begin" or name == "slow_edges":
             continue
-        phases.setdefault(name, []).append((ms, n))
+        if name == "fold_span":
+            spans.append((ms, n))
+            continue
+        phases.setdefault(name, []).append(ms)
         kernels.setdefault(kernel_of.get(name, name), []).append((ms, n))
+    avg_fold_s = (sum(ms for ms, _ in spans) / len(spans) / 1e3) if spans else float("nan")
+    avg_fold_edges = (sum(n for _, n in spans) / len(spans)) if spans else E1 / n_windows
+    pipeline_gbs = BYTES_PER_EDGE * avg_fold_edges / avg_fold_s / 1e9 if spans else None
+
+    def kernel_bytes(k, units):
+        """Algorithmic bytes of one launch: per edge for the edge kernels, per id otherwise."""
+        per = KERNEL_BYTES.get(k)
+        if per is None:
+            return None
+        return per[0] * (units if per[1] == "edge" else V)
+
+    kstats = {}
+    for k, v in kernels.items():
+        ms_avg = sum(ms for ms, _ in v) / len(v)
+        units = sum(n for _, n in v) / len(v)
+        by = kernel_bytes(k, units)
+        kstats[k] = {"launches_per_step": len(v) / max(1, inst_steps), "ms_avg": ms_avg,
+                     "ms_per_step": sum(ms for ms, _ in v) / max(1, inst_steps),
+                     "achieved_gbs": (by / (ms_avg / 1e3) / 1e9) if by and ms_avg > 0 else None}
     prof = profile_record(args.workload)
-    # the dominant kernel: the one the committed rocprof summary names for this workload, else the largest total
-    dominant = next((k for k in kernels if prof and k in prof.get("kernel", "")), None)
-    if dominant is None:
-        dominant = max(kernels, key=lambda k: sum(ms for ms, _ in kernels[k] if k != "compress_bits_kernel"))
-    dom_ms = sum(ms for ms, _ in kernels[dominant]) / len(kernels[dominant])
-    dom_edges = sum(n for _, n in kernels[dominant]) / len(kernels[dominant])
-    achieved = BYTES_PER_EDGE * dom_edges / (dom_ms / 1e3) / 1e9 if dom_edges else 0.0
+    # the dominant kernel: the largest device time per step
+    dominant = max(kstats, key=lambda k: kstats[k]["ms_per_step"]) if kstats else None
+    dom_ms = kstats[dominant]["ms_avg"] if dominant else float("nan")
+    dom_units = (sum(n for _, n in kernels[dominant]) / len(kernels[dominant])) if dominant else 0
+    achieved = kstats[dominant]["achieved_gbs"] if dominant else None
     traffic = None
-    if prof and dominant in prof.get("kernel", "") and abs(prof.get("edges_per_launch", 0) - dom_edges) <= 0.01 * dom_edges:
+    if prof and dominant and dominant in prof.get("kernel", "") and \
+            abs(prof.get("edges_per_launch", 0) - dom_units) <= 0.01 * max(1, dom_units):
         traffic = prof["hbm_bytes_per_launch"]
 
     merge_ms = [a.elapsed_time(b) for a, b in merge_events]
@@ -252,18 +288,21 @@ def main():
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": traffic,
             "traffic_unit": "bytes per launch",
             "traffic_source": (prof["source"] + f"; L2 hit rate {prof['l2_hit_rate']:.2f}") if traffic else None,
             "kernel_ms_avg": dom_ms,
-            "kernel_edges_per_launch": int(dom_edges),
-            "bytes_per_edge": BYTES_PER_EDGE,
-            "phases_ms_per_step": {k: sum(ms for ms, _ in v) / args.steps for k, v in phases.items()},
-            "kernel_launches_per_step": len(kernels[dominant]) / args.steps,
+            "kernel_units_per_launch": int(dom_units),
+            "bytes_per_unit": KERNEL_BYTES.get(dominant),
+            "timing": ("hipExtLaunchKernel dispatch events on the forest's stream, every timed step"
+                       if timed_inst else f"hipExtLaunchKernel dispatch events, {inst_steps} steps after the timed region"),
+            "kernels": kstats,
+            "phases_ms_per_step": {k: sum(v) / max(1, inst_steps) for k, v in phases.items()},
             "pipeline": {"fold_ms_avg": avg_fold_s * 1e3, "edges_per_fold": int(avg_fold_edges),
-                         "achieved": pipeline_gbs, "frac": pipeline_gbs / HBM_PEAK_GBS,
-                         "host_enqueue_ms_avg": sum(host_fold_s) / len(host_fold_s) * 1e3},
+                         "bytes_per_edge": BYTES_PER_EDGE, "achieved": pipeline_gbs,
+                         "frac": (pipeline_gbs / HBM_PEAK_GBS) if pipeline_gbs else None,
+                         "host_enqueue_ms_avg": (sum(host_fold_s) / len(host_fold_s) * 1e3) if host_fold_s else None},
         },
         "summary": {"seen": seen, "components": comps},
         "merge": ({"ms_avg": sum(merge_ms) / len(merge_ms), "last": group.last} if group is not None and merge_ms

@@ -21,6 +21,7 @@
 // every loop terminates. Path-splitting stores are plain stores to NON-root slots only (a slot once
 // non-root never becomes root again: all values written are < v), so they never race with a hook.
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -159,6 +160,21 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
     __shared__ u32 s_slow;
     const u32 bitmap_u32 = LDS ? nwords * 2 : 0;  // nwords = u64 words, even
     u64* ring = reinterpret_cast<u64*>(s_dyn + bitmap_u32) + (threadIdx.x >> 6) * kRing;
+    // split the batch into an aligned body of 16-B pairs of edges and a scalar head/tail
+    const u64 head = ((reinterpret_cast<uintptr_t>(edges) & 15) && n_edges) ? 1 : 0;
+    const u64 n2 = (n_edges - head) / 2;
+    const u32x4* body = reinterpret_cast<const u32x4*>(edges + head);
+    const u64 stride = (u64)gridDim.x * BLOCK;
+    const u32 lane = threadIdx.x & 63;
+    // Whole waves run both loops with the same trip count (the ring cursors wq/wd must stay wave-uniform):
+    // the loops are driven by the wave's first pair index, lanes past the end are predicated off.
+    u64 base = (u64)blockIdx.x * BLOCK + (threadIdx.x - lane);
+    u32x4 q[DEPTH];
+    const bool first_round = PIPE && base + 63 + (DEPTH - 1) * stride < n2;
+    if (first_round) {  // in flight while the bitmap is copied into LDS
+#pragma unroll
+        for (int k = 0; k < DEPTH; ++k) q[k] = __builtin_nontemporal_load(body + base + lane + k * stride);
+    }
     const u32* bm = bits;
     if (threadIdx.x == 0) s_slow = 0;
     if constexpr (LDS) {
@@ -170,22 +186,10 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
     __syncthreads();
     const u32 g = *giant;
     u32 wq = 0, wd = 0;  // this wave's ring: pushed / drained (wave-uniform)
-    // split the batch into an aligned body of 16-B pairs of edges and a scalar head/tail
-    const u64 head = ((reinterpret_cast<uintptr_t>(edges) & 15) && n_edges) ? 1 : 0;
-    const u64 n2 = (n_edges - head) / 2;
-    const u32x4* body = reinterpret_cast<const u32x4*>(edges + head);
-    const u64 stride = (u64)gridDim.x * BLOCK;
-    const u32 lane = threadIdx.x & 63;
-    // Whole waves run both loops with the same trip count (the ring cursors wq/wd must stay wave-uniform):
-    // the loops are driven by the wave's first pair index, lanes past the end are predicated off.
-    u64 base = (u64)blockIdx.x * BLOCK + (threadIdx.x - lane);
     if constexpr (PIPE) {
         // software-pipelined: the next DEPTH loads are in flight while this round is filtered (and while a
         // ring drain waits on its union chains)
-        if (base + 63 + (DEPTH - 1) * stride < n2) {
-            u32x4 q[DEPTH];
-#pragma unroll
-            for (int k = 0; k < DEPTH; ++k) q[k] = __builtin_nontemporal_load(body + base + lane + k * stride);
+        if (first_round) {
             while (true) {
                 const u64 nb = base + DEPTH * stride;
                 const bool more = nb + 63 + (DEPTH - 1) * stride < n2;  // wave-uniform
@@ -471,6 +475,22 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
                                                          u8* __restrict__ flags, u32* __restrict__ gmin) {
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     __shared__ u32 s_min;
+    constexpr int D = 8;  // 16-B edge pairs in flight per lane
+    auto ld = [](const u32x4* p) -> u32x4 {
+        if constexpr (NT) return __builtin_nontemporal_load(p);
+        else return *p;
+    };
+    // aligned body of 16-B edge pairs + scalar head/tail edges; this lane's pairs are i, i + stride, ...
+    const u64 head = ((reinterpret_cast<uintptr_t>(edges) & 15) && n) ? 1 : 0;
+    const u64 n2 = (n - head) / 2;
+    const u32x4* body = reinterpret_cast<const u32x4*>(edges + head);
+    const u64 stride = (u64)gridDim.x * BLOCK;
+    const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
+    const u64 cnt = i < n2 ? (n2 - 1 - i) / stride + 1 : 0;
+    u32x4 q[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k)  // the first round is in flight while the bitmap is copied into LDS
+        if ((u64)k < cnt) q[k] = ld(body + i + k * stride);
     u32* bm = const_cast<u32*>(bits32);
     if (threadIdx.x == 0) s_min = UNSEEN;
     if constexpr (LDS) {
@@ -493,30 +513,19 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
             }
         }
     };
-    auto ld = [](const u32x4* p) -> u32x4 {
-        if constexpr (NT) return __builtin_nontemporal_load(p);
-        else return *p;
-    };
-    // aligned body of 16-B edge pairs (four in flight per lane) + scalar head/tail edges
-    const u64 head = ((reinterpret_cast<uintptr_t>(edges) & 15) && n) ? 1 : 0;
-    const u64 n2 = (n - head) / 2;
-    const u32x4* body = reinterpret_cast<const u32x4*>(edges + head);
-    const u64 stride = (u64)gridDim.x * BLOCK;
-    u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
-    for (; i + 3 * stride < n2; i += 4 * stride) {
-        u32x4 q[4];
+    for (u64 r = 0; r < cnt; r += D) {  // software-pipelined: round r + D is loading while round r is visited
+        u32x4 nq[D];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = ld(body + i + k * stride);
+        for (int k = 0; k < D; ++k)
+            if (r + D + k < cnt) nq[k] = ld(body + i + (r + D + k) * stride);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            visit(q[k].x, q[k].y);
-            visit(q[k].z, q[k].w);
-        }
-    }
-    for (; i < n2; i += stride) {
-        const u32x4 q = ld(body + i);
-        visit(q.x, q.y);
-        visit(q.z, q.w);
+        for (int k = 0; k < D; ++k)
+            if (r + k < cnt) {
+                visit(q[k].x, q[k].y);
+                visit(q[k].z, q[k].w);
+            }
+#pragma unroll
+        for (int k = 0; k < D; ++k) q[k] = nq[k];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (head) visit((u32)edges[0], (u32)(edges[0] >> 32));
@@ -800,6 +809,7 @@ struct FoldTune {
     bool seed = true;
     int seed_passes = 2;
     u64 seed_div = 2;
+    u64 seed_div1 = 2;  // the first BFS pass covers 1/seed_div1 of the batch (>= 1/seed_div)
     double seed_refresh = 0;  // refresh point of a seeded batch (fraction; 0 = none)
     bool pipe = true;  // software-pipelined filtered stream (next round's loads in flight during filtering)
     u32 drain_at = 64;  // a wave drains its slow-edge ring once this many edges are pending (1..64)
@@ -849,13 +859,17 @@ struct gcc_forest {
     std::vector<u32> host_labels;
     bool host_valid = false;
 
-    int timing = 0;  // 1: events around the fold and its phases; 2: also slow-path edge counts
-    hipEvent_t t0 = nullptr, t1 = nullptr;
-    bool t_recorded = false;
-    // per-phase profile of the last fold (timing mode only): (phase name, event after it)
-    std::vector<std::pair<const char*, hipEvent_t>> prof;
-    std::vector<u64> prof_edges;  // edges processed by each profiled phase (0 for non-fold phases)
-    size_t prof_used = 0;
+    int timing = 0;  // 1: every pipeline kernel timed by its own dispatch (start/stop events); 2: + slow-edge counts
+    // timing mode: per-kernel log (name, event pair index or -1 for a fold's "begin" marker, edges processed)
+    struct KLog {
+        const char* name;
+        int ev;
+        u64 edges;
+    };
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> kev;  // event-pair pool, reused after each drain
+    size_t kev_used = 0;
+    std::vector<KLog> klog;
+    int last_fold_first = -1, last_fold_last = -1;  // event pairs spanning the last timed fold
     u32* h_segcount = nullptr;  // pinned copies of the slow-queue segment counts, one row per filtered round
     std::vector<u32> slow_rounds;
 
@@ -894,6 +908,36 @@ static void mark_mutated(gcc_forest* h) {
     h->compressed = false;
 }
 
+// Every kernel of the fold pipeline goes through launch_k. Timing mode launches it with hipExtLaunchKernelGGL's
+// start/stop events, which the runtime records from the dispatch itself: the logged duration is the kernel's
+// own execution, and no extra packets (hipEventRecord markers cost ~4 us each between dependent kernels) are
+// put between the pipeline's launches.
+template <typename F, typename... Args>
+static int launch_k(gcc_forest* h, const char* name, u64 edges, F kernel, dim3 grid, dim3 block, size_t shmem,
+                    Args... args) {
+    if (!h->timing) {
+        hipLaunchKernelGGL(kernel, grid, block, (unsigned)shmem, h->stream, args...);
+    } else {
+        if (h->klog.size() > 16384) {  // nobody drains the log: keep it bounded
+            h->klog.clear();
+            h->kev_used = 0;
+            h->last_fold_first = h->last_fold_last = -1;
+        }
+        if (h->kev_used == h->kev.size()) {
+            hipEvent_t a, b;
+            HIP_TRY(hipEventCreate(&a));
+            HIP_TRY(hipEventCreate(&b));
+            h->kev.push_back({a, b});
+        }
+        const int ev = (int)h->kev_used++;
+        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shmem, h->stream, h->kev[ev].first, h->kev[ev].second, 0,
+                              args...);
+        h->klog.push_back({name, ev, edges});
+    }
+    HIP_TRY(hipGetLastError());
+    return GCC_OK;
+}
+
 static int materialize_reset(gcc_forest* h) {
     if (!h->pending_reset) return GCC_OK;
     HIP_TRY(hipMemsetAsync(h->d_parent, 0xFF, (size_t)h->cap * sizeof(u32), h->stream));
@@ -909,49 +953,34 @@ static int alloc_filter(gcc_forest* h) {
 }
 
 // compress into the spare buffer and swap; with the filter on, refresh the giant bitmap from the new labels
-static int compress_now(gcc_forest* h) {
+static int compress_now(gcc_forest* h, const char* name = "compress") {
+    int rc = GCC_OK;
     if (!h->filter_enabled()) {
-        hipLaunchKernelGGL(compress_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent,
-                           h->d_spare, h->cap);
+        rc = launch_k(h, name, 0, compress_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->d_parent,
+                      h->d_spare, h->cap);
     } else {
-        int rc = alloc_filter(h);
+        rc = alloc_filter(h);
         if (rc) return rc;
         if (!h->has_giant)  // first refresh of this forest: elect the component to track
-            hipLaunchKernelGGL(giant_vote_kernel, dim3(1), dim3(1024), 0, h->stream, h->d_parent, h->cap,
-                               h->d_giant + h->giant_slot);
-        hipLaunchKernelGGL(compress_bits_kernel, dim3(grid_for(h->nwords() * 64ull, kMaxGrid)), dim3(kBlock), 0,
-                           h->stream, h->d_parent, h->d_spare, h->cap, h->d_giant + h->giant_slot,
-                           h->d_giant + (h->giant_slot ^ 1), h->d_bits);
+            rc = launch_k(h, "vote", 0, giant_vote_kernel, dim3(1), dim3(1024), 0, h->d_parent, h->cap,
+                          h->d_giant + h->giant_slot);
+        if (!rc)
+            rc = launch_k(h, name, 0, compress_bits_kernel, dim3(grid_for(h->nwords() * 64ull, kMaxGrid)), dim3(kBlock), 0,
+                          h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
+                          h->d_giant + (h->giant_slot ^ 1), h->d_bits);
         h->giant_slot ^= 1;
         h->has_giant = true;
     }
-    HIP_TRY(hipGetLastError());
+    if (rc) return rc;
     std::swap(h->d_parent, h->d_spare);
     h->compressed = true;
     return GCC_OK;
 }
 
-static int prof_mark(gcc_forest* h, const char* phase, u64 edges = 0) {
-    if (!h->timing) return GCC_OK;
-    if (h->prof_used == h->prof.size()) {
-        hipEvent_t ev;
-        HIP_TRY(hipEventCreate(&ev));
-        h->prof.push_back({phase, ev});
-        h->prof_edges.push_back(0);
-    }
-    h->prof[h->prof_used].first = phase;
-    h->prof_edges[h->prof_used] = edges;
-    HIP_TRY(hipEventRecord(h->prof[h->prof_used].second, h->stream));
-    h->prof_used++;
-    return GCC_OK;
-}
-
-static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n) {
+static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* name) {
     if (n == 0) return GCC_OK;
-    hipLaunchKernelGGL(fold_kernel, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent,
-                       reinterpret_cast<const u64*>(d_pairs), n);
-    HIP_TRY(hipGetLastError());
-    return GCC_OK;
+    return launch_k(h, name, n, fold_kernel, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent,
+                    reinterpret_cast<const u64*>(d_pairs), n);
 }
 
 static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
@@ -964,6 +993,7 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u32* bits = reinterpret_cast<const u32*>(h->d_bits);
     const u32* giant = h->d_giant + h->giant_slot;
     const int variant = (h->tune.depth == 8 ? 1 : 0) | (h->tune.pipe ? 2 : 0);
+    int rc = GCC_OK;
     if (lds) {
         const size_t lds_bytes = (size_t)nw * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64);
         static bool lds_attr_set = false;  // > 64 KiB of dynamic LDS must be allowed explicitly (once per process)
@@ -976,31 +1006,29 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
             for (const void* f : fns) HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
             lds_attr_set = true;
         }
-#define GCC_FILTERED(D, P)                                                                                       \
-    hipLaunchKernelGGL((fold_filtered_kernel<true, kFilterBlockLds, D, P>), dim3(nblocks), dim3(kFilterBlockLds), \
-                       lds_bytes, h->stream, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
+#define GCC_FILTERED(D, P)                                                                                     \
+    launch_k(h, "filtered", n, fold_filtered_kernel<true, kFilterBlockLds, D, P>, dim3(nblocks), dim3(kFilterBlockLds), \
+             lds_bytes, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
         switch (variant) {
-        case 0: GCC_FILTERED(4, false); break;
-        case 1: GCC_FILTERED(8, false); break;
-        case 2: GCC_FILTERED(4, true); break;
-        default: GCC_FILTERED(8, true); break;
+        case 0: rc = GCC_FILTERED(4, false); break;
+        case 1: rc = GCC_FILTERED(8, false); break;
+        case 2: rc = GCC_FILTERED(4, true); break;
+        default: rc = GCC_FILTERED(8, true); break;
         }
 #undef GCC_FILTERED
     } else {
         const size_t lds_bytes = (kBlock / 64) * kRing * sizeof(u64);
 #define GCC_FILTERED(D, P)                                                                                  \
-    hipLaunchKernelGGL((fold_filtered_kernel<false, kBlock, D, P>), dim3(nblocks), dim3(kBlock), lds_bytes, \
-                       h->stream, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
+    launch_k(h, "filtered", n, fold_filtered_kernel<false, kBlock, D, P>, dim3(nblocks), dim3(kBlock), lds_bytes, \
+             h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
         switch (variant) {
-        case 0: GCC_FILTERED(4, false); break;
-        case 1: GCC_FILTERED(8, false); break;
-        case 2: GCC_FILTERED(4, true); break;
-        default: GCC_FILTERED(8, true); break;
+        case 0: rc = GCC_FILTERED(4, false); break;
+        case 1: rc = GCC_FILTERED(8, false); break;
+        case 2: rc = GCC_FILTERED(4, true); break;
+        default: rc = GCC_FILTERED(8, true); break;
         }
 #undef GCC_FILTERED
     }
-    HIP_TRY(hipGetLastError());
-    int rc = prof_mark(h, "filtered", n);
     if (rc) return rc;
     if (h->timing > 1) {  // measurement only (profile mode): how many edges took the slow path
         if (!h->h_segcount) HIP_TRY(hipHostMalloc((void**)&h->h_segcount, 8 * kMaxGrid * sizeof(u32), hipHostMallocDefault));
@@ -1031,16 +1059,17 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
                                     (int)(2 * kHubSlots * sizeof(u32))));
         hub_attr = true;
     }
-    hipLaunchKernelGGL(seed_hub_kernel, dim3(hub_grid), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32), h->stream, edges,
-                       std::min(n, kHubSample), flags, bits, h->cap, gmin);
-    HIP_TRY(hipGetLastError());
-    rc = prof_mark(h, "seed_hub");
+    rc = launch_k(h, "seed_hub", 0, seed_hub_kernel, dim3(hub_grid), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32), edges,
+                  std::min(n, kHubSample), flags, bits, h->cap, gmin);
     if (rc) return rc;
     const u64 pref = std::min(n, std::max<u64>(t.filter_min_batch, n / std::max<u64>(1, t.seed_div)));
+    // the first pass only has to reach the hubs next to h: a shorter prefix
+    const u64 pref1 = std::min(pref, std::max<u64>(t.filter_min_batch, n / std::max<u64>(1, t.seed_div1)));
     const u32 nw32 = 2 * (h->nwords() + (h->nwords() & 1));  // u32 bitmap words, rounded to 16 B
     const bool lds = nw32 / 2 <= kLdsBitmapMaxWords;
     const unsigned pack_grid = grid_for(((u64)h->cap + 3) / 4, kMaxGrid);
     for (int p = 0; p < t.seed_passes; ++p) {
+        const u64 np = p == 0 ? pref1 : pref;
         if (lds) {
             static bool attr = false;
             if (!attr) {
@@ -1050,38 +1079,31 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
                                                 (int)(kLdsBitmapMaxWords * sizeof(u64))));
                 attr = true;
             }
-            if (t.seed_nt)
-                hipLaunchKernelGGL((seed_bfs_kernel<true, kFilterBlockLds, true>), dim3(h->n_cu), dim3(kFilterBlockLds),
-                                   (size_t)nw32 * sizeof(u32), h->stream, edges, pref, bits, nw32, flags, gmin);
-            else
-                hipLaunchKernelGGL((seed_bfs_kernel<true, kFilterBlockLds, false>), dim3(h->n_cu), dim3(kFilterBlockLds),
-                                   (size_t)nw32 * sizeof(u32), h->stream, edges, pref, bits, nw32, flags, gmin);
+            const size_t sh = (size_t)nw32 * sizeof(u32);
+            rc = t.seed_nt ? launch_k(h, "seed_bfs", np, seed_bfs_kernel<true, kFilterBlockLds, true>, dim3(h->n_cu),
+                                      dim3(kFilterBlockLds), sh, edges, np, (const u32*)bits, nw32, flags, gmin)
+                           : launch_k(h, "seed_bfs", np, seed_bfs_kernel<true, kFilterBlockLds, false>, dim3(h->n_cu),
+                                      dim3(kFilterBlockLds), sh, edges, np, (const u32*)bits, nw32, flags, gmin);
         } else {
-            const unsigned grid = grid_for((pref + 1) / 2, kMaxGrid);
-            if (t.seed_nt)
-                hipLaunchKernelGGL((seed_bfs_kernel<false, kBlock, true>), dim3(grid), dim3(kBlock), 0, h->stream, edges,
-                                   pref, bits, nw32, flags, gmin);
-            else
-                hipLaunchKernelGGL((seed_bfs_kernel<false, kBlock, false>), dim3(grid), dim3(kBlock), 0, h->stream, edges,
-                                   pref, bits, nw32, flags, gmin);
+            const unsigned grid = grid_for((np + 1) / 2, kMaxGrid);
+            rc = t.seed_nt ? launch_k(h, "seed_bfs", np, seed_bfs_kernel<false, kBlock, true>, dim3(grid), dim3(kBlock), 0,
+                                      edges, np, (const u32*)bits, nw32, flags, gmin)
+                           : launch_k(h, "seed_bfs", np, seed_bfs_kernel<false, kBlock, false>, dim3(grid), dim3(kBlock), 0,
+                                      edges, np, (const u32*)bits, nw32, flags, gmin);
         }
-        HIP_TRY(hipGetLastError());
-        rc = prof_mark(h, "seed_bfs", pref);
         if (rc) return rc;
         if (p + 1 < t.seed_passes) {
-            hipLaunchKernelGGL(seed_pack_kernel<false>, dim3(pack_grid), dim3(kBlock), 0, h->stream, h->d_parent, h->cap,
-                               flags, bits, gmin, h->d_giant + h->giant_slot);
-            HIP_TRY(hipGetLastError());
-            rc = prof_mark(h, "seed_pack");
+            rc = launch_k(h, "seed_pack", 0, seed_pack_kernel<false>, dim3(pack_grid), dim3(kBlock), 0, h->d_parent, h->cap,
+                          (const u8*)flags, bits, (const u32*)gmin, h->d_giant + h->giant_slot);
             if (rc) return rc;
         }
     }
-    hipLaunchKernelGGL(seed_pack_kernel<true>, dim3(pack_grid), dim3(kBlock), 0, h->stream, h->d_parent, h->cap, flags,
-                       bits, gmin, h->d_giant + h->giant_slot);
-    HIP_TRY(hipGetLastError());
+    rc = launch_k(h, "seed_init", 0, seed_pack_kernel<true>, dim3(pack_grid), dim3(kBlock), 0, h->d_parent, h->cap,
+                  (const u8*)flags, bits, (const u32*)gmin, h->d_giant + h->giant_slot);
+    if (rc) return rc;
     h->pending_reset = false;
     h->has_giant = true;
-    return prof_mark(h, "seed_init");
+    return GCC_OK;
 }
 
 // The fold pipeline for one batch (UpdateCC.foldEdges over the batch, DisjointSet.union per edge):
@@ -1095,12 +1117,8 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
 static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (n == 0) return GCC_OK;
     const FoldTune& t = h->tune;
-    if (h->timing) {
-        HIP_TRY(hipEventRecord(h->t0, h->stream));
-        if (h->prof_used > 4096) h->prof_used = 0;  // nobody drains the log: keep it bounded
-        int rc0 = prof_mark(h, "begin");
-        if (rc0) return rc0;
-    }
+    const int ev_first = (int)h->kev_used;
+    if (h->timing) h->klog.push_back({"begin", -1, 0});
     int rc = GCC_OK;
     u64 b = 0;
     // seeding pays when the BFS lookups are LDS-resident; beyond that (C4: 8 MiB bitmap) the sampled start
@@ -1118,19 +1136,16 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
     }
     if (rc) return rc;
     if (!h->filter_enabled() || (!h->has_giant && n < t.filter_min_batch)) {
-        rc = launch_plain(h, d_pairs, n);
+        rc = launch_plain(h, d_pairs, n, "plain");
         b = n;
-        if (!rc) rc = prof_mark(h, "plain", n);
     } else if (!h->has_giant) {
         const u64 s_end = std::min(n, std::max<u64>(t.filter_min_batch / 4, n / std::max<u64>(1, t.sample_div)));
         for (u64 c = std::max<u64>(1, t.sample_first); b < s_end && !rc; c *= std::max<u64>(2, t.sample_growth)) {
             const u64 e = std::min(s_end, b + c);
-            rc = launch_plain(h, d_pairs + 2 * b, e - b);
-            if (!rc) rc = prof_mark(h, "sample", e - b);
+            rc = launch_plain(h, d_pairs + 2 * b, e - b, "sample");
             b = e;
         }
-        if (!rc && b < n) rc = compress_now(h);
-        if (!rc) rc = prof_mark(h, "refresh");
+        if (!rc && b < n) rc = compress_now(h, "refresh");
     }
     int next_refresh = 0;
     while (!rc && b < n) {
@@ -1142,15 +1157,14 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
         rc = launch_filtered(h, d_pairs + 2 * b, e - b);
         b = e;
         if (!rc && b < n) {
-            rc = compress_now(h);
-            if (!rc) rc = prof_mark(h, "refresh");
+            rc = compress_now(h, "refresh");
             ++next_refresh;
         }
     }
     if (rc) return rc;
-    if (h->timing) {
-        HIP_TRY(hipEventRecord(h->t1, h->stream));
-        h->t_recorded = true;
+    if (h->timing && (int)h->kev_used > ev_first) {
+        h->last_fold_first = ev_first;
+        h->last_fold_last = (int)h->kev_used - 1;
     }
     mark_mutated(h);
     return GCC_OK;
@@ -1317,9 +1331,6 @@ static int forest_create_impl(int device, uint32_t id_capacity, uint32_t* d_buf0
         if (e == hipSuccess) e = hipMalloc((void**)&h->d_spare, (size_t)id_capacity * sizeof(u32));
         if (e != hipSuccess) return fail(set_err(GCC_E_OOM, "hipMalloc 2 x u32[%u]: %s", id_capacity, hipGetErrorString(e)));
     }
-    e = hipEventCreate(&h->t0);
-    if (e == hipSuccess) e = hipEventCreate(&h->t1);
-    if (e != hipSuccess) return fail(set_err(GCC_E_HIP, "hipEventCreate: %s", hipGetErrorString(e)));
     rc = gcc_forest_reset(h);
     if (rc) return fail(rc);
     *out = h;
@@ -1354,10 +1365,11 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (h->d_giant) (void)hipFree(h->d_giant);
     if (h->d_qcount) (void)hipFree(h->d_qcount);
     if (h->d_counts) (void)hipFree(h->d_counts);
-    for (auto& pe : h->prof) (void)hipEventDestroy(pe.second);
+    for (auto& pe : h->kev) {
+        (void)hipEventDestroy(pe.first);
+        (void)hipEventDestroy(pe.second);
+    }
     if (h->h_segcount) (void)hipHostFree(h->h_segcount);
-    if (h->t0) (void)hipEventDestroy(h->t0);
-    if (h->t1) (void)hipEventDestroy(h->t1);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
     return GCC_OK;
@@ -1684,7 +1696,6 @@ int gcc_forest_import_pairs(gcc_forest* h, const uint32_t* pairs, uint64_t n_pai
 int gcc_forest_enable_timing(gcc_forest* h, int enable) {
     CHECK_ARG(h, "null forest");
     h->timing = enable < 0 ? 0 : (enable > 2 ? 2 : enable);
-    h->t_recorded = false;
     return GCC_OK;
 }
 
@@ -1709,6 +1720,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "seed_global") t.seed_global = value != 0;
     else if (k == "seed_passes") t.seed_passes = std::max(0, std::min(16, (int)value));
     else if (k == "seed_div") t.seed_div = std::max<u64>(1, (u64)value);
+    else if (k == "seed_div1") t.seed_div1 = std::max<u64>(1, (u64)value);
     else if (k == "seed_refresh") t.seed_refresh = value;
     else return set_err(GCC_E_INVALID, "unknown tuning key '%s'", key);
     return GCC_OK;
@@ -1717,21 +1729,51 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
 int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size) {
     CHECK_ARG(h && buf && size > 0, "null argument");
     buf[0] = 0;
-    if (!h->t_recorded || h->prof_used == 0) return GCC_OK;  // nothing logged
+    if (h->klog.empty()) return GCC_OK;  // nothing logged
     DeviceGuard g(h->device);
-    HIP_TRY(hipEventSynchronize(h->t1));
+    HIP_TRY(hipStreamSynchronize(h->stream));
     std::string out;
-    char line[128];
-    hipEvent_t prev = h->t0;
-    for (size_t i = 0; i < h->prof_used; ++i) {
+    char line[160];
+    // per kernel: "name ms edges"; per fold: a "begin" line first and, after its kernels, "fold_span ms edges" =
+    // first kernel start -> last kernel stop (the fold's device time including the gaps between its launches)
+    int first = -1, last = -1;
+    u64 fold_edges = 0;
+    auto close_fold = [&]() {
+        if (first >= 0 && last >= 0) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, h->kev[first].first, h->kev[last].second);
+            snprintf(line, sizeof line, "fold_span %.5f %llu\n", ms, (unsigned long long)fold_edges);
+            out += line;
+        }
+        first = last = -1;
+        fold_edges = 0;
+    };
+    bool in_fold = false;
+    for (const auto& k : h->klog) {
+        if (k.ev < 0) {  // a fold starts
+            if (in_fold) close_fold();
+            in_fold = true;
+            out += "begin 0 0\n";
+            continue;
+        }
         float ms = 0;
-        if (i > 0 && std::strcmp(h->prof[i].first, "begin") != 0)
-            HIP_TRY(hipEventElapsedTime(&ms, prev, h->prof[i].second));
-        snprintf(line, sizeof line, "%s %.4f %llu\n", h->prof[i].first, ms, (unsigned long long)h->prof_edges[i]);
+        HIP_TRY(hipEventElapsedTime(&ms, h->kev[k.ev].first, h->kev[k.ev].second));
+        snprintf(line, sizeof line, "%s %.5f %llu\n", k.name, ms, (unsigned long long)k.edges);
         out += line;
-        prev = h->prof[i].second;
+        if (in_fold && std::strcmp(k.name, "compress") != 0) {  // kernels enqueued by this fold
+            if (first < 0) first = k.ev;
+            last = k.ev;
+            if (!std::strcmp(k.name, "filtered") || !std::strcmp(k.name, "plain") || !std::strcmp(k.name, "sample"))
+                fold_edges += k.edges;
+        } else if (in_fold) {
+            close_fold();
+            in_fold = false;
+        }
     }
-    h->prof_used = 0;  // drained
+    if (in_fold) close_fold();
+    h->klog.clear();  // drained: the event pairs are reused
+    h->kev_used = 0;
+    h->last_fold_first = h->last_fold_last = -1;
     for (size_t r = 0; r < h->slow_rounds.size(); ++r) {
         unsigned long long sum = 0;
         for (u32 b = 0; b < h->slow_rounds[r]; ++b) sum += h->h_segcount[r * kMaxGrid + b];
@@ -1746,10 +1788,10 @@ int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size) {
 
 int gcc_forest_last_fold_ms(gcc_forest* h, float* ms) {
     CHECK_ARG(h && ms, "null argument");
-    CHECK_ARG(h->t_recorded, "no timed fold recorded (call gcc_forest_enable_timing first)");
+    CHECK_ARG(h->last_fold_first >= 0, "no timed fold recorded (call gcc_forest_enable_timing first)");
     DeviceGuard g(h->device);
-    HIP_TRY(hipEventSynchronize(h->t1));
-    HIP_TRY(hipEventElapsedTime(ms, h->t0, h->t1));
+    HIP_TRY(hipEventSynchronize(h->kev[h->last_fold_last].second));
+    HIP_TRY(hipEventElapsedTime(ms, h->kev[h->last_fold_first].first, h->kev[h->last_fold_last].second));
     return GCC_OK;
 }
 

@@ -324,6 +324,13 @@ def test_fold_timing_events():
     ds.enable_timing(1)
     ds.fold(G.generate_host(cfg))
     assert ds.last_fold_ms() > 0.0
+    log = ds.fold_profile()  # per-kernel dispatch timings + one span per fold
+    names = [k for k, _, _ in log]
+    assert names[0] == "begin" and "fold_span" in names and "filtered" in names
+    span = [ms for k, ms, _ in log if k == "fold_span"][0]
+    kernels = sum(ms for k, ms, _ in log if k not in ("begin", "fold_span", "slow_edges", "compress"))
+    assert 0 < kernels <= span * 1.001
+    assert [n for k, _, n in log if k == "fold_span"][0] == E
 
 
 # ---- cross-GPU merge message (include/gelly_cc.h): encode / absorb, the RCCL payload's two ends ----

@@ -16,14 +16,8 @@ from gelly_stream import generators as G  # noqa: E402
 
 CONFIGS = [
     ("default", {}),
-    ("noseed", {"seed": 0}),
-    ("drain32", {"drain_at": 32}),
-    ("drain16", {"drain_at": 16}),
-    ("drain8", {"drain_at": 8}),
-    ("seednt0", {"seed_nt": 0}),
-    ("seednt0_d16", {"seed_nt": 0, "drain_at": 16}),
-    ("p2div4_d16", {"seed_div": 4, "drain_at": 16}),
-    ("p3div4_d16", {"seed_div": 4, "seed_passes": 3, "drain_at": 16}),
+    ("nopipe", {"pipe": 0}),
+    ("depth8", {"depth": 8}),
 ]
 
 
