@@ -272,6 +272,7 @@ def main():
                 "c2_rmat20": "R-MAT scale 20 (A,B,C,D=0.57,0.19,0.19,0.05), edge factor 16, seeded permutation",
                 "c3_gnm24": "uniform G(n,m) n=2^24 m=9227469",
                 "c4_kron26": "Kronecker scale 26, edge factor 16",
+                "c4_share": "Kronecker scale 26, 2^27 edges per GPU of C4's stream (x8 GPUs = C4's 2^30 edges)",
                 "c5_adversarial": "shuffled 2^23-path + 1024 stars of 8192",
             }.get(base.name, base.name),
             "edges_per_gpu": E1,

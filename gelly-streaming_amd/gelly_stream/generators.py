@@ -53,6 +53,9 @@ CONFIGS = {
     "c3_gnm24": StreamConfig("c3_gnm24", native.GCC_GEN_GNM, n_vertices=1 << 24, n_edges=9_227_469, seed=SEED_BASE | 3),
     # C4: Kronecker scale 26, edge factor 16 (1 GiB-edge stream over 8 GPUs)
     "c4_kron26": StreamConfig("c4_kron26", native.GCC_GEN_RMAT, scale=26, n_edges=16 << 26, seed=SEED_BASE | 4),
+    # C4's per-GPU share: the first 2^27 edges of the C4 stream (same seed, counter-based generator), all 2^26
+    # ids. Weak-scaled over W ranks (bench.py) it is the first W * 2^27 edges: W = 8 is exactly C4.
+    "c4_share": StreamConfig("c4_share", native.GCC_GEN_RMAT, scale=26, n_edges=2 << 26, seed=SEED_BASE | 4),
     # C5: adversarial path over 2^23 ids + 1024 stars of 8192 ids, windows of 2^16 edges
     "c5_adversarial": StreamConfig("c5_adversarial", native.GCC_GEN_ADVERSARIAL, scale=23, n_stars=1024,
                                    star_size=8192, seed=SEED_BASE | 5, window_edges=1 << 16),

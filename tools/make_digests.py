@@ -14,7 +14,7 @@ PATH = os.path.join(ROOT, "tools", "digests.json")
 
 
 def main():
-    names = sys.argv[1:] or ["c2_rmat20", "c3_gnm24", "c5_adversarial", "c4_kron26"]
+    names = sys.argv[1:] or ["c2_rmat20", "c3_gnm24", "c5_adversarial", "c4_kron26", "c4_share"]
     out = json.load(open(PATH)) if os.path.exists(PATH) else {}
     for wl in names:
         cfg = G.CONFIGS[wl]
