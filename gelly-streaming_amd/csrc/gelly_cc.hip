@@ -149,9 +149,57 @@ __device__ __forceinline__ void filter_edge(bool valid, u32 a, u32 b, const u32*
     ring_push(valid && !(ia & ib), ia ? g : a, ib ? g : b, ring, wq, wd, parent, drain_at);
 }
 
+// A round of N edges of the filtered stream with the direct hook (HOOK): an edge with exactly one end in C and
+// the other end b > g is folded by ONE atomicMin(parent[b], g), issued for the whole round before any result
+// is looked at. old = UNSEEN (b was new: the common case), b (b was a root) or g: b now hangs under g, done.
+// Otherwise b left the tree of old, or already hung under something smaller: (g, old) goes to the ring, whose
+// union restores the connection. Every write still lowers a parent, so the forest stays a forest and roots stay
+// minimal (b's descendants are all > b > g). Other non-skipped edges take the ring as in filter_edge.
+// The hooks' results are checked one round later (HookCarry): the atomics' latency overlaps the next round's
+// loads and filtering instead of stalling the wave.
+template <int N>
+struct HookCarry {
+    u32 other[N], old[N];
+    bool hook[N];
+    __device__ __forceinline__ void clear() {
+#pragma unroll
+        for (int k = 0; k < N; ++k) hook[k] = false;
+    }
+    __device__ __forceinline__ void settle(u32 g, u64* ring, u32& wq, u32& wd, u32* parent, u32 drain_at) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const bool again = hook[k] && old[k] != GCC_UNSEEN && old[k] != other[k] && old[k] != g;
+            ring_push(again, g, again ? old[k] : 0u, ring, wq, wd, parent, drain_at);
+        }
+    }
+};
+
+template <bool LDS, int N>
+__device__ __forceinline__ void filter_round(const bool* valid, const u32* a, const u32* b, const u32* bm, u32 g,
+                                             u64* ring, u32& wq, u32& wd, u32* parent, u32 drain_at,
+                                             HookCarry<N>& carry) {
+    HookCarry<N> cur;
+    bool slow[N];
+    u32 pa[N], pb[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const u32 ia = in_c<LDS>(bm, a[k]), ib = in_c<LDS>(bm, b[k]);
+        cur.other[k] = ia ? b[k] : a[k];
+        cur.hook[k] = valid[k] && (ia ^ ib) && cur.other[k] > g;
+        slow[k] = valid[k] && !(ia & ib) && !cur.hook[k];
+        pa[k] = ia ? g : a[k];
+        pb[k] = ib ? g : b[k];
+        if (cur.hook[k]) cur.old[k] = atomicMin(&parent[cur.other[k]], g);
+    }
+    carry.settle(g, ring, wq, wd, parent, drain_at);  // the previous round's hooks (their atomics have returned)
+#pragma unroll
+    for (int k = 0; k < N; ++k) ring_push(slow[k], pa[k], pb[k], ring, wq, wd, parent, drain_at);
+    carry = cur;
+}
+
 // Dynamic LDS: [bitmap (LDS variant), 16-B aligned][BLOCK/64 rings of kRing u64]. slow_count[blockIdx.x] =
 // the block's slow edges (measurement).
-template <bool LDS, int BLOCK, int DEPTH, bool PIPE>
+template <bool LDS, int BLOCK, int DEPTH, bool PIPE, bool HOOK>
 __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
                                                               u64 n_edges, const u32* __restrict__ bits, u32 nwords,
                                                               const u32* __restrict__ giant,
@@ -186,6 +234,10 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
     __syncthreads();
     const u32 g = *giant;
     u32 wq = 0, wd = 0;  // this wave's ring: pushed / drained (wave-uniform)
+    HookCarry<2 * DEPTH> carry;  // HOOK: the last round's atomicMin results, settled one round later
+    HookCarry<2> carry2;
+    carry.clear();
+    carry2.clear();
     if constexpr (PIPE) {
         // software-pipelined: the next DEPTH loads are in flight while this round is filtered (and while a
         // ring drain waits on its union chains)
@@ -198,10 +250,24 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
 #pragma unroll
                     for (int k = 0; k < DEPTH; ++k) nq[k] = __builtin_nontemporal_load(body + nb + lane + k * stride);
                 }
+                if constexpr (HOOK) {
+                    bool vv[2 * DEPTH];
+                    u32 ea[2 * DEPTH], eb[2 * DEPTH];
 #pragma unroll
-                for (int k = 0; k < DEPTH; ++k) {
-                    filter_edge<LDS>(true, q[k].x, q[k].y, bm, g, ring, wq, wd, parent, drain_at);
-                    filter_edge<LDS>(true, q[k].z, q[k].w, bm, g, ring, wq, wd, parent, drain_at);
+                    for (int k = 0; k < DEPTH; ++k) {
+                        vv[2 * k] = vv[2 * k + 1] = true;
+                        ea[2 * k] = q[k].x;
+                        eb[2 * k] = q[k].y;
+                        ea[2 * k + 1] = q[k].z;
+                        eb[2 * k + 1] = q[k].w;
+                    }
+                    filter_round<LDS, 2 * DEPTH>(vv, ea, eb, bm, g, ring, wq, wd, parent, drain_at, carry);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < DEPTH; ++k) {
+                        filter_edge<LDS>(true, q[k].x, q[k].y, bm, g, ring, wq, wd, parent, drain_at);
+                        filter_edge<LDS>(true, q[k].z, q[k].w, bm, g, ring, wq, wd, parent, drain_at);
+                    }
                 }
                 base = nb;
                 if (!more) break;
@@ -227,8 +293,18 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
         const bool valid = i < n2;
         u32x4 q = {0, 0, 0, 0};
         if (valid) q = __builtin_nontemporal_load(body + i);
-        filter_edge<LDS>(valid, q.x, q.y, bm, g, ring, wq, wd, parent, drain_at);
-        filter_edge<LDS>(valid, q.z, q.w, bm, g, ring, wq, wd, parent, drain_at);
+        if constexpr (HOOK) {
+            const bool vv[2] = {valid, valid};
+            const u32 ea[2] = {q.x, q.z}, eb[2] = {q.y, q.w};
+            filter_round<LDS, 2>(vv, ea, eb, bm, g, ring, wq, wd, parent, drain_at, carry2);
+        } else {
+            filter_edge<LDS>(valid, q.x, q.y, bm, g, ring, wq, wd, parent, drain_at);
+            filter_edge<LDS>(valid, q.z, q.w, bm, g, ring, wq, wd, parent, drain_at);
+        }
+    }
+    if constexpr (HOOK) {  // the last rounds' hooks
+        carry.settle(g, ring, wq, wd, parent, drain_at);
+        carry2.settle(g, ring, wq, wd, parent, drain_at);
     }
     NoCount c;
     // the rest of this wave's ring (< 64 + 64 entries)
@@ -811,7 +887,7 @@ struct FoldTune {
     u64 seed_div = 2;
     u64 seed_div1 = 2;  // the first BFS pass covers 1/seed_div1 of the batch (>= 1/seed_div)
     double seed_refresh = 0;  // refresh point of a seeded batch (fraction; 0 = none)
-    bool pipe = true;  // software-pipelined filtered stream (next round's loads in flight during filtering)
+    bool hook = true;  // direct atomicMin hook of (T, new id) edges in the filtered stream (filter_round)
     u32 drain_at = 64;  // a wave drains its slow-edge ring once this many edges are pending (1..64)
     bool seed_nt = true;  // non-temporal loads in the BFS passes (false: the prefix may stay in the MALL)
     bool seed_global = false;  // also seed when the bitmap does not fit LDS (global-bitmap BFS lookups)
@@ -992,23 +1068,25 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
     const u32* bits = reinterpret_cast<const u32*>(h->d_bits);
     const u32* giant = h->d_giant + h->giant_slot;
-    const int variant = (h->tune.depth == 8 ? 1 : 0) | (h->tune.pipe ? 2 : 0);
+    // instantiated variants: depth 4 with / without the direct hook, depth 8 without; software-pipelined stream
+    // depth 8 with the hook carry exceeds 128 VGPRs (1024-thread blocks) and spills: it runs without the hook
+    const int variant = h->tune.depth == 8 ? 1 : (h->tune.hook ? 2 : 0);
     int rc = GCC_OK;
     if (lds) {
         const size_t lds_bytes = (size_t)nw * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64);
         static bool lds_attr_set = false;  // > 64 KiB of dynamic LDS must be allowed explicitly (once per process)
         if (!lds_attr_set) {
             const int max_lds = (int)(kLdsBitmapMaxWords * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64));
-            const void* fns[4] = {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, false>,
-                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, false>,
-                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true>,
-                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true>};
+            const void* fns[4] = {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, false>,
+                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true, false>,
+                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, true>,
+                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true, true>};
             for (const void* f : fns) HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
             lds_attr_set = true;
         }
-#define GCC_FILTERED(D, P)                                                                                     \
-    launch_k(h, "filtered", n, fold_filtered_kernel<true, kFilterBlockLds, D, P>, dim3(nblocks), dim3(kFilterBlockLds), \
-             lds_bytes, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
+#define GCC_FILTERED(D, H)                                                                                     \
+    launch_k(h, "filtered", n, fold_filtered_kernel<true, kFilterBlockLds, D, true, H>, dim3(nblocks),         \
+             dim3(kFilterBlockLds), lds_bytes, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
         switch (variant) {
         case 0: rc = GCC_FILTERED(4, false); break;
         case 1: rc = GCC_FILTERED(8, false); break;
@@ -1018,9 +1096,9 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
 #undef GCC_FILTERED
     } else {
         const size_t lds_bytes = (kBlock / 64) * kRing * sizeof(u64);
-#define GCC_FILTERED(D, P)                                                                                  \
-    launch_k(h, "filtered", n, fold_filtered_kernel<false, kBlock, D, P>, dim3(nblocks), dim3(kBlock), lds_bytes, \
-             h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
+#define GCC_FILTERED(D, H)                                                                                  \
+    launch_k(h, "filtered", n, fold_filtered_kernel<false, kBlock, D, true, H>, dim3(nblocks), dim3(kBlock), \
+             lds_bytes, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
         switch (variant) {
         case 0: rc = GCC_FILTERED(4, false); break;
         case 1: rc = GCC_FILTERED(8, false); break;
@@ -1714,7 +1792,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "refresh3") t.refresh[2] = value;
     else if (k == "depth") t.depth = (int)value == 8 ? 8 : 4;
     else if (k == "seed") t.seed = value != 0;
-    else if (k == "pipe") t.pipe = value != 0;
+    else if (k == "hook") t.hook = value != 0;
     else if (k == "drain_at") t.drain_at = (u32)std::max(1.0, std::min(64.0, value));
     else if (k == "seed_nt") t.seed_nt = value != 0;
     else if (k == "seed_global") t.seed_global = value != 0;

@@ -3,7 +3,8 @@
 HBM bytes per launch of a kernel = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: FETCH_SIZE/WRITE_SIZE are KB, and on
 gfx950 FETCH_SIZE reports half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section). The 2x is
 exact for the 16-B/lane edge stream and uncalibrated for the random 4-B parent reads (an upper estimate there).
-Usage: python tools/pmc_summary.py <pmc_dir> <workload> <kernel substring> <edges_per_launch> <out.json>"""
+Usage: python tools/pmc_summary.py <pmc_dir> <workload> <kernel substring> <units_per_launch> <bytes_per_unit> <out.json>
+(units: edges for the edge kernels; bytes_per_unit: bench.py KERNEL_BYTES)"""
 import csv
 import json
 import sys
@@ -19,7 +20,8 @@ def per_kernel(path, counter):
 
 
 def main():
-    d, workload, ksub, edges, out = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    d, workload, ksub, edges, per, out = (sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), float(sys.argv[5]),
+                                          sys.argv[6])
     f = per_kernel(f"{d}/fetch/run_counter_collection.csv", "FETCH_SIZE")
     w = per_kernel(f"{d}/write/run_counter_collection.csv", "WRITE_SIZE")
     h = per_kernel(f"{d}/hit/run_counter_collection.csv", "TCC_HIT_sum")
@@ -36,11 +38,15 @@ def main():
         "fetch_size_kb": fetch_kb,
         "write_size_kb": write_kb,
         "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
-        "algorithmic_bytes_per_launch": 16 * edges,
+        "bytes_per_unit": per,
+        "algorithmic_bytes_per_launch": per * edges,
         "l2_hit_rate": hit / (hit + miss),
         "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum,TCC_MISS_sum (separate passes), "
                   f"bench.py --steps 5; bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch",
     }
+    rec["all_kernels"] = {  # every kernel of the run: HBM bytes per launch (same correction)
+        k: {"launches": len(f[k]), "hbm_bytes_per_launch": (2 * sum(f[k]) / len(f[k]) + (sum(w[k]) / len(w[k]) if w.get(k) else 0)) * 1024}
+        for k in f}
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
