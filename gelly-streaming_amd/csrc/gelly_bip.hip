@@ -1,0 +1,290 @@
+// gelly_bip.hip — gfx950 signed forest: the device summary of BipartitenessCheck (include/gelly_cc.h, gcc_signed_*).
+//
+// What it replaces (`…/` = src/main/java/org/apache/flink/graph/streaming/):
+//   Candidates (Tuple2<Boolean, TreeMap<Long, Map<Long, SignedVertex>>>)   …/summaries/Candidates.java:27-197
+//   BipartitenessCheck.updateFunction.foldEdges = candidates.merge(edgeToCandidate(v1, v2))
+//                                                                         …/library/BipartitenessCheck.java:54-61, :93-95
+//   BipartitenessCheck.combineFunction.reduce  = c1.merge(c2)            :128-130
+// A Candidates object is a set of components, each a map vertex -> sign with the two ends of every edge on
+// opposite signs, plus a success flag that turns false (for good) once an edge closes an odd cycle. Signs are
+// only defined up to one flip per component (Candidates.merge reverses the input side to match), so the parity
+// contract observes, per vertex: its component's minimum id and its sign relative to that vertex, plus the flag.
+//
+// Device representation: one u32 word[id_capacity] per forest + one fail word.
+//   word[v] == GCC_UNSEEN          -> v is not in any component
+//   word[v] == (p << 1) | q        -> v hangs under p with sign(v) = sign(p) XOR q   (q = parity bit)
+//   p == v (then q == 0)           -> v is a root
+// Invariant p <= v (min-id hooking, as the CC forest): roots are component minima, and a compress leaves
+// (min id << 1) | parity-to-min, which IS the canonical output. Ids must be < 2^31 - 1 (word range).
+// Concurrency follows the CC forest (gelly_cc.hip header): a word only ever points to an ancestor, with the
+// parity of the path to it, so a stale read is historically valid; roots leave root state only through CAS;
+// path-splitting plain stores only target non-roots. The parity of a vertex relative to any ancestor is a
+// fact of the constraints, never changed by later writes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "abi_common.h"
+#include "gelly_cc.h"
+#include "signed_uf.h"  // find / seen / unite, shared with the host replay (tests/cpp/test_signed_uf.cpp)
+
+namespace {
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+constexpr u32 kUnseen = GCC_UNSEEN;
+constexpr u32 kMaxSignedId = 0x7FFFFFFEu;  // (id << 1) | 1 must stay below GCC_UNSEEN
+constexpr unsigned kMaxGrid = 2048;
+
+__device__ __forceinline__ u32 sw_parent(u32 w) { return suf::parent_of(w); }
+__device__ __forceinline__ u32 sw_par(u32 w) { return suf::parity_of(w); }
+__device__ __forceinline__ u32 sfind(u32* word, u32 x, u32 wx, u32& par) { return suf::find(word, x, wx, par); }
+__device__ __forceinline__ u32 sseen(u32* word, u32 v) { return suf::seen(word, v); }
+__device__ __forceinline__ void sunite(u32* word, u32 u, u32 v, u32 q, u32* fail) { suf::unite(word, u, v, q, fail); }
+
+__global__ __launch_bounds__(256) void signed_fold_kernel(u32* __restrict__ word, const u64* __restrict__ edges, u64 n,
+                                                         u32* __restrict__ fail) {
+    const u64 stride = (u64)gridDim.x * 256;
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const u64 e = __builtin_nontemporal_load(edges + i);
+        sunite(word, (u32)e, (u32)(e >> 32), 1u, fail);
+    }
+}
+
+// into ∪= the signed partition of `other` (any forest of the same id range, compressed or not): the triple
+// (v, parent, parity) of every seen v is the constraint sign(v) XOR sign(parent) = parity. A failed input
+// fails the result (Candidates.merge :78-81).
+__global__ __launch_bounds__(256) void signed_merge_kernel(u32* __restrict__ word, const u32* __restrict__ other, u32 n,
+                                                          u32* __restrict__ fail, const u32* __restrict__ other_fail) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && *other_fail) *fail = 1u;
+    const u64 stride = (u64)gridDim.x * 256;
+    for (u64 v = (u64)blockIdx.x * 256 + threadIdx.x; v < n; v += stride) {
+        const u32 w = other[v];
+        if (w == kUnseen) continue;
+        const u32 p = sw_parent(w);
+        if (p == (u32)v) {
+            (void)sseen(word, (u32)v);
+            continue;
+        }
+        sunite(word, (u32)v, p, sw_par(w), fail);
+    }
+}
+
+// canonical words, out of place (as the CC compress): (min id << 1) | parity to it, UNSEEN stays UNSEEN
+__global__ __launch_bounds__(256) void signed_compress_kernel(u32* __restrict__ word, u32* __restrict__ out, u32 n) {
+    const u64 stride = (u64)gridDim.x * 256;
+    for (u64 v = (u64)blockIdx.x * 256 + threadIdx.x; v < n; v += stride) {
+        const u32 w = word[v];
+        if (w == kUnseen || sw_parent(w) == (u32)v) {  // a separate launch: no stale reads of word[v] itself
+            out[v] = w;
+            continue;
+        }
+        u32 par;
+        const u32 r = sfind(word, (u32)v, w, par);
+        out[v] = (r << 1) | par;
+    }
+}
+
+}  // namespace
+
+struct gcc_signed {
+    int device = 0;
+    u32 cap = 0;
+    u32* d_word = nullptr;
+    u32* d_spare = nullptr;
+    u32* d_fail = nullptr;
+    u32* d_stage = nullptr;  // host-fed edges
+    u64 stage_cap = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    bool compressed = true;
+    std::vector<u32> host_words;
+    bool host_valid = false;
+};
+
+static int signed_compress(gcc_signed* h) {
+    if (h->compressed) return GCC_OK;
+    hipLaunchKernelGGL(signed_compress_kernel, dim3(grid_for_n(h->cap, kMaxGrid)), dim3(256), 0, h->stream, h->d_word,
+                       h->d_spare, h->cap);
+    HIP_TRY(hipGetLastError());
+    std::swap(h->d_word, h->d_spare);
+    h->compressed = true;
+    return GCC_OK;
+}
+
+// fold a device batch. The first launches are small and grow geometrically: while the hubs of a skewed stream
+// are still unhooked, few threads contend on their roots (the CC forest's sampled start, gelly_cc.hip).
+static int signed_fold(gcc_signed* h, const u32* d_pairs, u64 n) {
+    const u64* edges = reinterpret_cast<const u64*>(d_pairs);
+    u64 b = 0;
+    for (u64 c = 4096; b < n; c *= 4) {
+        const u64 e = std::min(n, b + c);
+        hipLaunchKernelGGL(signed_fold_kernel, dim3(grid_for_n(e - b, kMaxGrid)), dim3(256), 0, h->stream, h->d_word,
+                           edges + b, e - b, h->d_fail);
+        HIP_TRY(hipGetLastError());
+        b = e;
+    }
+    h->compressed = false;
+    h->host_valid = false;
+    return GCC_OK;
+}
+
+extern "C" {
+
+int gcc_signed_create(int device, uint32_t id_capacity, gcc_signed** out) {
+    CHECK_ARG(out, "out is null");
+    *out = nullptr;
+    CHECK_ARG(id_capacity >= 1 && id_capacity <= kMaxSignedId + 1, "id_capacity must be in [1, 2^31 - 1]");
+    int rc = gcc_check_device(device);
+    if (rc) return rc;
+    DeviceGuard g(device);
+    gcc_signed* h = new gcc_signed();
+    h->device = device;
+    h->cap = id_capacity;
+    hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->d_word, (size_t)id_capacity * sizeof(u32));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->d_spare, (size_t)id_capacity * sizeof(u32));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->d_fail, sizeof(u32));
+    if (e != hipSuccess) {
+        gcc_signed_destroy(h);
+        return gcc_set_err(e == hipErrorOutOfMemory ? GCC_E_OOM : GCC_E_HIP, "gcc_signed_create: %s",
+                           hipGetErrorString(e));
+    }
+    h->stream = h->own_stream;
+    rc = gcc_signed_reset(h);
+    if (rc) {
+        gcc_signed_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return GCC_OK;
+}
+
+int gcc_signed_destroy(gcc_signed* h) {
+    if (!h) return GCC_OK;
+    DeviceGuard g(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->d_word) (void)hipFree(h->d_word);
+    if (h->d_spare) (void)hipFree(h->d_spare);
+    if (h->d_fail) (void)hipFree(h->d_fail);
+    if (h->d_stage) (void)hipFree(h->d_stage);
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    delete h;
+    return GCC_OK;
+}
+
+int gcc_signed_set_stream(gcc_signed* h, void* hip_stream, int use_own) {
+    CHECK_ARG(h, "null handle");
+    DeviceGuard g(h->device);
+    hipStream_t next = use_own ? h->own_stream : (hipStream_t)hip_stream;
+    if (next != h->stream) {
+        hipEvent_t ev;
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ev, h->stream));
+        HIP_TRY(hipStreamWaitEvent(next, ev, 0));
+        HIP_TRY(hipEventDestroy(ev));
+        h->stream = next;
+    }
+    return GCC_OK;
+}
+
+int gcc_signed_reset(gcc_signed* h) {
+    CHECK_ARG(h, "null handle");
+    DeviceGuard g(h->device);
+    HIP_TRY(hipMemsetAsync(h->d_word, 0xFF, (size_t)h->cap * sizeof(u32), h->stream));
+    HIP_TRY(hipMemsetAsync(h->d_fail, 0, sizeof(u32), h->stream));
+    h->compressed = true;
+    h->host_valid = false;
+    return GCC_OK;
+}
+
+int gcc_signed_fold_device(gcc_signed* h, const uint32_t* d_pairs, uint64_t n_edges) {
+    CHECK_ARG(h, "null handle");
+    CHECK_ARG(d_pairs || n_edges == 0, "d_pairs is null");
+    if (n_edges == 0) return GCC_OK;
+    DeviceGuard g(h->device);
+    return signed_fold(h, d_pairs, n_edges);
+}
+
+int gcc_signed_fold_host(gcc_signed* h, const uint32_t* pairs, uint64_t n_edges) {
+    CHECK_ARG(h, "null handle");
+    CHECK_ARG(pairs || n_edges == 0, "pairs is null");
+    if (n_edges == 0) return GCC_OK;
+    for (u64 i = 0; i < 2 * n_edges; ++i)  // a bad id would be an out-of-bounds device access
+        if (pairs[i] >= h->cap) return gcc_set_err(GCC_E_INVALID, "vertex id %u >= id_capacity %u", pairs[i], h->cap);
+    DeviceGuard g(h->device);
+    if (h->stage_cap < n_edges) {
+        if (h->d_stage) {
+            HIP_TRY(hipStreamSynchronize(h->stream));
+            HIP_TRY(hipFree(h->d_stage));
+            h->d_stage = nullptr;
+        }
+        HIP_TRY(hipMalloc((void**)&h->d_stage, n_edges * 2 * sizeof(u32)));
+        h->stage_cap = n_edges;
+    }
+    HIP_TRY(hipMemcpyAsync(h->d_stage, pairs, n_edges * 2 * sizeof(u32), hipMemcpyHostToDevice, h->stream));
+    int rc = signed_fold(h, h->d_stage, n_edges);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(h->stream));  // pageable source: consumed before returning
+    return GCC_OK;
+}
+
+int gcc_signed_merge(gcc_signed* into, gcc_signed* from) {
+    CHECK_ARG(into && from, "null handle");
+    if (into == from) return GCC_OK;
+    CHECK_ARG(from->cap <= into->cap, "merge source has a larger id range than the target");
+    CHECK_ARG(from->device == into->device, "signed forests must live on one device");
+    DeviceGuard g(into->device);
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ev, from->stream));
+    HIP_TRY(hipStreamWaitEvent(into->stream, ev, 0));
+    hipLaunchKernelGGL(signed_merge_kernel, dim3(grid_for_n(from->cap, kMaxGrid)), dim3(256), 0, into->stream,
+                       into->d_word, from->d_word, from->cap, into->d_fail, from->d_fail);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev, into->stream));
+    HIP_TRY(hipStreamWaitEvent(from->stream, ev, 0));  // from must not change before the merge has read it
+    HIP_TRY(hipEventDestroy(ev));
+    into->compressed = false;
+    into->host_valid = false;
+    return GCC_OK;
+}
+
+int gcc_signed_words(gcc_signed* h, uint32_t* out, uint32_t n) {
+    CHECK_ARG(h, "null handle");
+    CHECK_ARG(out || n == 0, "out is null");
+    CHECK_ARG(n <= h->cap, "n exceeds id_capacity");
+    DeviceGuard g(h->device);
+    if (!h->host_valid) {
+        int rc = signed_compress(h);
+        if (rc) return rc;
+        h->host_words.resize(h->cap);
+        HIP_TRY(hipMemcpyAsync(h->host_words.data(), h->d_word, (size_t)h->cap * sizeof(u32), hipMemcpyDeviceToHost,
+                               h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        h->host_valid = true;
+    }
+    std::memcpy(out, h->host_words.data(), (size_t)n * sizeof(u32));
+    return GCC_OK;
+}
+
+int gcc_signed_success(gcc_signed* h, int* success) {
+    CHECK_ARG(h && success, "null argument");
+    DeviceGuard g(h->device);
+    u32 f = 0;
+    HIP_TRY(hipMemcpyAsync(&f, h->d_fail, sizeof(u32), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    *success = f ? 0 : 1;
+    return GCC_OK;
+}
+
+int gcc_signed_capacity(gcc_signed* h, uint32_t* id_capacity) {
+    CHECK_ARG(h && id_capacity, "null argument");
+    *id_capacity = h->cap;
+    return GCC_OK;
+}
+
+}  // extern "C"

@@ -32,6 +32,7 @@
 #include <string>
 #include <vector>
 
+#include "abi_common.h"
 #include "edge_gen.h"
 #include "gelly_cc.h"
 #include "uf_device.h"
@@ -46,8 +47,7 @@ typedef uint64_t u64;
 // ------------------------------------------------------------------------------------------------
 static thread_local std::string g_last_error;
 
-static int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-static int set_err(int code, const char* fmt, ...) {
+int gcc_set_err(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -57,19 +57,7 @@ static int set_err(int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIP_TRY(expr)                                                                                  \
-    do {                                                                                               \
-        hipError_t e_ = (expr);                                                                        \
-        if (e_ != hipSuccess) {                                                                        \
-            return set_err(e_ == hipErrorOutOfMemory ? GCC_E_OOM : GCC_E_HIP, "%s failed: %s (%s:%d)", \
-                           #expr, hipGetErrorString(e_), __FILE__, __LINE__);                          \
-        }                                                                                              \
-    } while (0)
-
-#define CHECK_ARG(cond, msg)                               \
-    do {                                                   \
-        if (!(cond)) return set_err(GCC_E_INVALID, "%s", msg); \
-    } while (0)
+#define set_err gcc_set_err  // HIP_TRY / CHECK_ARG / DeviceGuard: abi_common.h
 
 // ------------------------------------------------------------------------------------------------
 // kernels
@@ -955,19 +943,7 @@ struct gcc_forest {
     bool filter_enabled() const { return tune.filter && cap >= kFilterMinIds; }
 };
 
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
-static int check_device(int device) {
+int gcc_check_device(int device) {
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= 0) return set_err(GCC_E_NODEV, "no HIP device visible (%s)", hipGetErrorString(e));
@@ -1336,7 +1312,7 @@ int gcc_device_count(int* n) {
 }
 
 int gcc_init(int device) {
-    int rc = check_device(device);
+    int rc = gcc_check_device(device);
     if (rc) return rc;
     DeviceGuard g(device);
     HIP_TRY(hipFree(nullptr));
@@ -1382,7 +1358,7 @@ static int forest_create_impl(int device, uint32_t id_capacity, uint32_t* d_buf0
     CHECK_ARG(out, "out is null");
     *out = nullptr;
     CHECK_ARG(id_capacity >= 1 && id_capacity <= UNSEEN, "id_capacity must be in [1, 0xFFFFFFFF]");
-    int rc = check_device(device);
+    int rc = gcc_check_device(device);
     if (rc) return rc;
     DeviceGuard g(device);
     gcc_forest* h = new gcc_forest();

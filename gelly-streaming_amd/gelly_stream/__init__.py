@@ -8,14 +8,16 @@ Public surface mirrors the reference's operator API (`…/` = src/main/java/org/
   SimpleEdgeStream         …/SimpleEdgeStream.java            (constructor + aggregate())
 All device work goes through libgelly_cc.so (include/gelly_cc.h); there is no CPU fallback.
 """
-from .aggregation import EdgeBatch, EdgesFold, Merger, ReduceFunction, SummaryAggregation, SummaryBulkAggregation
+from .aggregation import (EdgeBatch, EdgesFold, Merger, ReduceFunction, SummaryAggregation, SummaryBulkAggregation,
+                          SummaryTreeReduce)
+from .bipartite import BipartitenessCheck, Candidates, SignedVertex
 from .edgestream import SimpleEdgeStream
-from .library import CombineCC, ConnectedComponents, UpdateCC
+from .library import CombineCC, ConnectedComponents, ConnectedComponentsTree, UpdateCC
 from .native import UNSEEN, GellyCCError, device_count
 from .summaries import DisjointSet
 
 __all__ = [
-    "CombineCC", "ConnectedComponents", "DisjointSet", "EdgeBatch", "EdgesFold", "GellyCCError", "Merger",
-    "ReduceFunction", "SimpleEdgeStream", "SummaryAggregation", "SummaryBulkAggregation", "UNSEEN", "UpdateCC",
-    "device_count",
+    "BipartitenessCheck", "Candidates", "CombineCC", "ConnectedComponents", "ConnectedComponentsTree", "DisjointSet",
+    "EdgeBatch", "EdgesFold", "GellyCCError", "Merger", "ReduceFunction", "SignedVertex", "SimpleEdgeStream",
+    "SummaryAggregation", "SummaryBulkAggregation", "SummaryTreeReduce", "UNSEEN", "UpdateCC", "device_count",
 ]

@@ -167,3 +167,45 @@ class SummaryBulkAggregation(SummaryAggregation[S, T]):
                 acc = self.group.reduce(acc, self.getCombineFun())
             out = merger.flatMap(acc)  # flatMap(Merger).setParallelism(1)
             yield self._transform(out) if self._transform else out
+
+
+class SummaryTreeReduce(SummaryBulkAggregation[S, T]):
+    """SummaryTreeReduce (…/SummaryTreeReduce.java:47-160): the window's partials are combined in a pairwise tree
+    instead of one all-to-one reduce. enhance() (:95-123) re-keys partition p to p // 2 and reduces each pair,
+    halving the parallelism until it is <= 2; timeWindowAll(...).reduce + Merger finish (:87-90).
+
+    degree: partitions of the window fold (-1 = the stream's parallelism, :75). On the device each partial is
+    its own summary, and every level of the tree is a set of independent pairwise combines (the cross-GPU
+    form of the same tree is ForestGroup's single all_gather, distributed.py).
+    """
+
+    def __init__(self, updateFun: EdgesFold[S], combineFun: ReduceFunction[S], initialVal: Callable[[], S],
+                 timeMillis: int, transientState: bool, degree: int = -1,
+                 transformFun: Optional[Callable[[S], T]] = None):
+        super().__init__(updateFun, combineFun, initialVal, timeMillis, transientState, transformFun)
+        self.degree = int(degree)
+
+    def run(self, edgeStream) -> Iterator[T]:
+        merger = self.getAggregator()
+        for window_batches in edgeStream.windows(self.timeMillis):
+            # map(PartitionMapper).setParallelism(degree).keyBy(0).timeWindow(t).fold(...) (:77-82)
+            partials: list[tuple[int, S]] = []
+            for p, batch in enumerate(window_batches):
+                if batch.n:
+                    partials.append((p, self.getUpdateFun().foldEdgeBatch(self.getInitialValue(), batch)))
+            if not partials:
+                continue
+            parallelism = max(len(window_batches), 1)
+            # enhance(): keyBy(f0 / 2) + AggregationWrapper reduce, while the parallelism is > 2 (:97-122)
+            while parallelism > 2:
+                pairs: dict[int, S] = {}
+                for key, s in partials:
+                    k = key // 2
+                    pairs[k] = s if k not in pairs else self.getCombineFun().reduce(pairs[k], s)
+                partials = sorted(pairs.items())
+                parallelism //= 2
+            acc = partials[0][1]
+            for _, s in partials[1:]:  # timeWindowAll(...).reduce(combineFun) (:88-89)
+                acc = self.getCombineFun().reduce(acc, s)
+            out = merger.flatMap(acc)
+            yield self._transform(out) if self._transform else out

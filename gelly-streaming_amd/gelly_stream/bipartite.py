@@ -1,0 +1,209 @@
+"""BipartitenessCheck and its Candidates summary on an MI355X (mirror of …/library/BipartitenessCheck.java and
+…/summaries/Candidates.java; `…/` = src/main/java/org/apache/flink/graph/streaming/).
+
+Reference:
+  BipartitenessCheck(long mergeWindowTime)   BipartitenessCheck.java:50-52
+      = SummaryBulkAggregation(new updateFunction(), new combineFunction(), new Candidates(true), t, false)
+  edgeToCandidate(v1, v2)                    :54-61   component min(v1,v2): {min: +, max: -}
+  updateFunction.foldEdges(c, v1, v2, ev)    :93-95   c.merge(edgeToCandidate(v1, v2))
+  combineFunction.reduce(c1, c2)             :128-130 c1.merge(c2)
+  Candidates = (success, TreeMap<component, Map<vertex, SignedVertex>>)   Candidates.java:27-197
+      merge: components that share a vertex are joined, the input side's signs reversed to match; a sign
+      conflict (an odd cycle) turns the result into fail() = (false, {}) for good (:78-81, :118-121, :194-196)
+
+Here the state is one device-resident signed forest (csrc/gelly_bip.hip): per vertex (parent, parity). The
+observable output is canonical: each component keyed by its minimum vertex, every sign relative to that vertex
+(the minimum is `true`). Signs in the reference depend on merge order (the input side is the one reversed), but
+within a component they always agree with ours up to one flip; toString() equals the reference's output whenever
+the reference's minimum vertex carries `true` (as in its own BipartitenessCheckTest). Two observable
+differences, both where the reference is order-dependent or loses information:
+  * a self loop (v, v) only adds v, as in the reference (edgeToCandidate ignores add()'s false, :58-59);
+  * Candidates.merge drops the result of a failed second-level merge (:128-131 call fail() without returning
+    it), so the reference can report success for a graph with an odd cycle closed across two merged summaries;
+    this summary reports the failure.
+"""
+from __future__ import annotations
+
+from collections.abc import Mapping
+from ctypes import byref, c_int, c_void_p
+from typing import Iterator, NamedTuple, Optional
+
+import numpy as np
+
+from .aggregation import EdgeBatch, EdgesFold, ReduceFunction, SummaryBulkAggregation
+from .native import UNSEEN, call
+
+
+class SignedVertex(NamedTuple):
+    """SignedVertex = Tuple2<Long, Boolean> (…/util/SignedVertex.java:23-41)."""
+
+    vertex: int
+    sign: bool
+
+    def getVertex(self) -> int:
+        return self.vertex
+
+    def getSign(self) -> bool:
+        return self.sign
+
+    def reverse(self) -> "SignedVertex":
+        return SignedVertex(self.vertex, not self.sign)
+
+    def __str__(self) -> str:  # Flink Tuple2.toString
+        return f"({self.vertex},{'true' if self.sign else 'false'})"
+
+
+class Candidates:
+    """Candidates backed by a device signed forest (Candidates.java:27-197)."""
+
+    def __init__(self, id_capacity: int, device: int = 0, success: bool = True):
+        """``new Candidates(true)`` (:31-34). success=False builds the failed value (fail(), :194-196)."""
+        self.id_capacity = int(id_capacity)
+        self.device = int(device)
+        h = c_void_p()
+        call("gcc_signed_create", self.device, self.id_capacity, byref(h))
+        self._h = h
+        self._words: Optional[np.ndarray] = None
+        self._failed_by_ctor = not success
+
+    # ---- lifetime ----
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            call("gcc_signed_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> c_void_p:
+        if not self._h:
+            raise ValueError("Candidates is closed")
+        return self._h
+
+    def _dirty(self) -> None:
+        self._words = None
+
+    # ---- Candidates.java surface ----
+    def getSuccess(self) -> bool:
+        """:44-46"""
+        if self._failed_by_ctor:
+            return False
+        ok = c_int()
+        call("gcc_signed_success", self.handle, byref(ok))
+        return bool(ok.value)
+
+    def getMap(self) -> dict[int, dict[int, SignedVertex]]:
+        """:48-50 — TreeMap component -> (TreeMap vertex -> SignedVertex); empty once failed (fail() = (false, {}))."""
+        if not self.getSuccess():
+            return {}
+        w = self.words()
+        seen = np.flatnonzero(w != UNSEEN)
+        out: dict[int, dict[int, SignedVertex]] = {}
+        for v in seen.tolist():
+            c, q = int(w[v]) >> 1, int(w[v]) & 1
+            out.setdefault(c, {})[v] = SignedVertex(v, q == 0)
+        return dict(sorted((c, dict(sorted(m.items()))) for c, m in out.items()))
+
+    def merge(self, other: "Candidates") -> "Candidates":
+        """:77-139 — self := self ∪ other (signs joined through shared vertices); returns self."""
+        if other._failed_by_ctor:
+            self._failed_by_ctor = True
+        call("gcc_signed_merge", self.handle, other.handle)
+        self._dirty()
+        return self
+
+    def toString(self) -> str:
+        """Flink Tuple2.toString of (success, TreeMap): e.g. ``(true,{1={1=(1,true), 2=(2,false)}})``."""
+        if not self.getSuccess():
+            return "(false,{})"
+        comps = ", ".join(f"{c}={{" + ", ".join(f"{v}={sv}" for v, sv in m.items()) + "}"
+                          for c, m in self.getMap().items())
+        return "(true,{" + comps + "})"
+
+    def __str__(self) -> str:
+        return self.toString()
+
+    # ---- batch / device extensions ----
+    def fold(self, pairs: np.ndarray) -> None:
+        """Fold host edges ((n, 2) u32): updateFunction.foldEdges over a whole batch."""
+        a = np.ascontiguousarray(pairs, dtype=np.uint32).reshape(-1)
+        call("gcc_signed_fold_host", self.handle, a.ctypes.data, a.size // 2)
+        self._dirty()
+
+    def fold_device(self, d_pairs: int, n_edges: int) -> None:
+        call("gcc_signed_fold_device", self.handle, c_void_p(d_pairs), int(n_edges))
+        self._dirty()
+
+    def reset(self) -> None:
+        call("gcc_signed_reset", self.handle)
+        self._failed_by_ctor = False
+        self._dirty()
+
+    def set_stream(self, hip_stream: Optional[int]) -> None:
+        call("gcc_signed_set_stream", self.handle, c_void_p(hip_stream or 0), 1 if hip_stream is None else 0)
+
+    def words(self) -> np.ndarray:
+        """Canonical words: (component min id << 1) | (sign differs from the minimum's), UNSEEN if unseen."""
+        if self._words is None:
+            out = np.empty(self.id_capacity, dtype=np.uint32)
+            call("gcc_signed_words", self.handle, out.ctypes.data, self.id_capacity)
+            self._words = out
+        return self._words
+
+
+class updateFunction(EdgesFold[Candidates]):
+    """BipartitenessCheck.updateFunction (:74-96)."""
+
+    def foldEdges(self, candidates: Candidates, v1: int, v2: int, edgeVal=None) -> Candidates:
+        candidates.fold(np.array([[v1, v2]], dtype=np.uint32))
+        return candidates
+
+    def foldEdgeBatch(self, candidates: Candidates, batch: EdgeBatch) -> Candidates:
+        if batch.host is not None:
+            candidates.fold(batch.host)
+        else:
+            candidates.fold_device(batch.device_ptr, batch.n)
+        return candidates
+
+
+class combineFunction(ReduceFunction[Candidates]):
+    """BipartitenessCheck.combineFunction (:108-131)."""
+
+    def reduce(self, c1: Candidates, c2: Candidates) -> Candidates:
+        return c1.merge(c2)
+
+
+class BipartitenessCheck(SummaryBulkAggregation[Candidates, Candidates]):
+    """BipartitenessCheck<K, EV> (BipartitenessCheck.java:39-52) on an MI355X."""
+
+    def __init__(self, mergeWindowTime: int, id_capacity: int, device: int = 0):
+        super().__init__(updateFunction(), combineFunction(), lambda: Candidates(id_capacity, device),
+                         mergeWindowTime, False)
+        self.id_capacity = id_capacity
+        self.device = device
+
+    @staticmethod
+    def edgeToCandidate(v1: int, v2: int, id_capacity: int, device: int = 0) -> Candidates:
+        """:54-61"""
+        c = Candidates(id_capacity, device)
+        c.fold(np.array([[v1, v2]], dtype=np.uint32))
+        return c
+
+    def run(self, edgeStream) -> Iterator[Candidates]:
+        """Fused SummaryBulkAggregation.run: with transientState=false the summary after window w is the merge of
+        every window's partial, whose canonical value is that of folding all edges so far into one forest."""
+        summary: Optional[Candidates] = None
+        for window_batches in edgeStream.windows(self.timeMillis):
+            n = 0
+            for batch in window_batches:
+                if batch.n:
+                    if summary is None:
+                        summary = self.getInitialValue()
+                    self.getUpdateFun().foldEdgeBatch(summary, batch)
+                    n += batch.n
+            if n:
+                yield summary

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 from typing import Iterator, Optional
 
-from .aggregation import EdgeBatch, EdgesFold, ReduceFunction, SummaryBulkAggregation
+from .aggregation import EdgeBatch, EdgesFold, ReduceFunction, SummaryBulkAggregation, SummaryTreeReduce
 from .summaries import DisjointSet
 
 
@@ -80,3 +80,15 @@ class ConnectedComponents(SummaryBulkAggregation[DisjointSet, DisjointSet]):
             elif n == 0:
                 continue
             yield summary
+
+
+class ConnectedComponentsTree(SummaryTreeReduce[DisjointSet, DisjointSet]):
+    """ConnectedComponentsTree<K, EV> (…/library/ConnectedComponentsTree.java:26-36): the CC summary with the
+    window's partial forests combined by SummaryTreeReduce's pairwise tree (degree partitions per window).
+    The emitted partition equals ConnectedComponents' (CombineCC is associative and commutative on it)."""
+
+    def __init__(self, mergeWindowTime: int, id_capacity: int, degree: int = -1, device: int = 0):
+        super().__init__(UpdateCC(), CombineCC(), lambda: DisjointSet(id_capacity, device), mergeWindowTime, False,
+                         degree)
+        self.id_capacity = id_capacity
+        self.device = device

@@ -89,6 +89,17 @@ _SIGS = {
     "gcc_forest_encode": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_forest_absorb": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_forest_absorb_many": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_uint64]),
+    # BipartitenessCheck's Candidates summary (signed forest)
+    "gcc_signed_create": (c_int, [c_int, c_uint32, POINTER(c_void_p)]),
+    "gcc_signed_destroy": (c_int, [c_void_p]),
+    "gcc_signed_set_stream": (c_int, [c_void_p, c_void_p, c_int]),
+    "gcc_signed_capacity": (c_int, [c_void_p, POINTER(c_uint32)]),
+    "gcc_signed_reset": (c_int, [c_void_p]),
+    "gcc_signed_fold_host": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_signed_fold_device": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_signed_merge": (c_int, [c_void_p, c_void_p]),
+    "gcc_signed_words": (c_int, [c_void_p, c_void_p, c_uint32]),
+    "gcc_signed_success": (c_int, [c_void_p, POINTER(c_int)]),
 }
 
 MSG_HEADER_BYTES = 16  # GCC_MSG_HEADER_BYTES

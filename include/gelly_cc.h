@@ -131,6 +131,25 @@ int gcc_forest_absorb(gcc_forest* h, const void* d_msg, uint64_t cap_others);
 int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_bytes, uint32_t count, uint32_t skip,
                            uint64_t cap_others);
 
+/* ---- BipartitenessCheck's summary: Candidates (…/summaries/Candidates.java:27-197) as a signed forest ----
+ * BipartitenessCheck(mergeWindowTime) = SummaryBulkAggregation(updateFunction, combineFunction, new Candidates(true),
+ * mergeWindowTime, false) (…/library/BipartitenessCheck.java:50-52). Per vertex the canonical word is
+ * (min id of its component << 1) | (its sign differs from that vertex's), GCC_UNSEEN if unseen; the success flag
+ * turns 0 for good once an edge closes an odd cycle (Candidates.fail, :194-196). Ids < 2^31 - 1. */
+typedef struct gcc_signed gcc_signed;
+int gcc_signed_create(int device, uint32_t id_capacity, gcc_signed** out); /* new Candidates(true) (:31-34) */
+int gcc_signed_destroy(gcc_signed* h);
+int gcc_signed_set_stream(gcc_signed* h, void* hip_stream, int use_own);
+int gcc_signed_capacity(gcc_signed* h, uint32_t* id_capacity);
+int gcc_signed_reset(gcc_signed* h);
+/* updateFunction.foldEdges = merge(edgeToCandidate(v1, v2)) per edge (BipartitenessCheck.java:54-61, :93-95) */
+int gcc_signed_fold_host(gcc_signed* h, const uint32_t* pairs, uint64_t n_edges);
+int gcc_signed_fold_device(gcc_signed* h, const uint32_t* d_pairs, uint64_t n_edges);
+/* combineFunction.reduce = Candidates.merge (BipartitenessCheck.java:128-130, Candidates.java:77-139) */
+int gcc_signed_merge(gcc_signed* into, gcc_signed* from);
+int gcc_signed_words(gcc_signed* h, uint32_t* out, uint32_t n); /* canonical words of ids [0, n) */
+int gcc_signed_success(gcc_signed* h, int* success);              /* Candidates.getSuccess (:44-46) */
+
 /* ---- summary reads (DisjointSet.find :71-85, getMatches :49-51; the emitted summary per window) ---- */
 int gcc_forest_compress(gcc_forest* h); /* async: canonical labels; afterwards gcc_forest_device_ptr = labels */
 int gcc_forest_labels(gcc_forest* h, uint32_t* out, uint32_t n); /* compress + copy n labels to host */

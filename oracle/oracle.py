@@ -50,6 +50,9 @@ def lib():
         l.orc_cc_stream.restype = c_int
         l.orc_cc_stream.argtypes = [c_void_p, c_uint64, c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_double)]
+        # bip_oracle.c (BipartitenessCheck / Candidates)
+        l.bo_stream.restype = c_int
+        l.bo_stream.argtypes = [c_void_p, c_void_p, c_uint32, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p]
         _lib = l
     return _lib
 
@@ -128,3 +131,19 @@ def cc_stream(pairs: np.ndarray, window_starts, V: int, partitions: int = 1, thr
     if labels is not None:
         out["labels"] = labels
     return out
+
+
+def bip_stream(pairs: np.ndarray, window_starts, V: int, partitions: int = 1) -> dict:
+    """BipartitenessCheck over an edge stream (bip_oracle.c): per window emitted, success and the canonical words
+    ((component min << 1) | sign differs from the min's; UNSEEN if absent), shape (W, V)."""
+    p = np.ascontiguousarray(pairs, dtype=np.uint32).reshape(-1)
+    ws = np.ascontiguousarray(window_starts, dtype=np.uint64)
+    W = ws.size - 1
+    emitted = np.zeros(W, dtype=np.uint8)
+    success = np.zeros(W, dtype=np.uint8)
+    words = np.zeros((W, V), dtype=np.uint32)
+    rc = lib().bo_stream(p.ctypes.data, ws.ctypes.data, W, partitions, V, emitted.ctypes.data, success.ctypes.data,
+                         words.ctypes.data)
+    if rc:
+        raise ValueError("oracle: a vertex id is >= V")
+    return {"emitted": emitted.astype(bool), "success": success.astype(bool), "words": words}

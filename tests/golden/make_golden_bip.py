@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Golden fixtures for BipartitenessCheck (tests/golden/bip_*.json). Run in the build container, not at test time.
+
+Independent of the C oracle and of libgelly_cc:
+  1. A literal pure-Python restatement of the reference's Candidates (…/summaries/Candidates.java:27-197: the
+     TreeMap of components, add(), merge() with the reversal of the input side, fail()), edgeToCandidate and the
+     fold / combine functions (…/library/BipartitenessCheck.java:54-61, :93-95, :128-130), over the
+     SummaryBulkAggregation window topology (…/SummaryBulkAggregation.java:76-83 + Merger).
+  2. The reference's own tests replayed on it: BipartitenessCheckTest (expected line
+     "(true,{1={1=(1,true), 2=(2,false), 3=(3,false), 4=(4,false), 5=(5,true), 7=(7,true), 9=(9,true)}})") and
+     NonBipartitnessCheckTest ("(false,{})"), src/test/java/org/apache/flink/graph/streaming/example/test/.
+  3. Every window cross-checked against networkx (is_bipartite per component, the components themselves).
+  4. Canonical output per window: success, and per vertex (component min << 1) | (sign differs from the min's).
+The literal restatement reproduces the KATs exactly, but Candidates.merge is not a partition join in general:
+_merge adds the input's vertices under min(inputKey, selfKey) (Candidates.java:176-189) without moving the self
+component when the input key is the smaller one, leaving overlapping "components"; and a failed second-level
+merge is dropped (:128-131). So the random streams are pinned by networkx (bipartite iff no odd cycle; per
+component its minimum vertex and a 2-colouring relative to it), and each window records whether the literal
+restatement happens to agree.
+Usage: python tests/golden/make_golden_bip.py
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import networkx as nx
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+UNSEEN = 0xFFFFFFFF
+
+
+class PyCandidates:
+    """Literal restatement of Candidates (dict = TreeMap/Map; sorted where the reference iterates a TreeMap)."""
+
+    def __init__(self, success=True):
+        self.success = success
+        self.map = {}  # component key -> {vertex: sign}
+
+    def add(self, component, vertex, sign):  # :61-74
+        comp = self.map.setdefault(component, {})
+        if vertex in comp and comp[vertex] != sign:
+            return False
+        comp[vertex] = sign
+        return True
+
+    def add_all(self, component, vertices):  # :52-59
+        for v, s in vertices.items():
+            if not self.add(component, v, s):
+                return False
+        return True
+
+    def merge(self, inp):  # :77-139
+        if not inp.success or not self.success:
+            return PyCandidates(False)
+        for in_key in sorted(inp.map):
+            in_comp = inp.map[in_key]
+            merge_with = []
+            for self_key in sorted(self.map):
+                self_comp = self.map[self_key]
+                if set(in_comp) == set(self_comp):
+                    continue
+                for v in in_comp:
+                    if v in self_comp:
+                        if self_key not in merge_with:
+                            merge_with.append(self_key)
+                            break
+            if not merge_with:
+                self.add_all(in_key, in_comp)
+            else:
+                merge_with.sort()
+                first = merge_with[0]
+                if not self._merge(inp, self, in_key, first):
+                    return PyCandidates(False)
+                first = min(in_key, first)
+                for k in merge_with[1:]:
+                    self._merge(self, self, k, first)  # :128-131: the result is dropped (reference behaviour)
+                    self.map.pop(k, None)
+        return self
+
+    @staticmethod
+    def _merge(inp, cand, in_key, self_key):  # :142-192
+        in_comp = inp.map[in_key]
+        self_comp = cand.map[self_key]
+        merge_by = [v for v in in_comp if v in self_comp]
+        reversed_ = in_comp[merge_by[0]] != self_comp[merge_by[0]]
+        for v in merge_by:
+            ok = (in_comp[v] != self_comp[v]) if reversed_ else (in_comp[v] == self_comp[v])
+            if not ok:
+                return False
+        common = min(in_key, self_key)
+        for v, s in list(in_comp.items()):
+            if not cand.add(common, v, (not s) if reversed_ else s):
+                return False
+        return True
+
+    def to_string(self):  # Tuple2.toString of (Boolean, TreeMap<Long, TreeMap<Long, SignedVertex>>)
+        if not self.success:
+            return "(false,{})"
+        comps = ", ".join(f"{c}={{" + ", ".join(f"{v}=({v},{'true' if s else 'false'})" for v, s in
+                                                sorted(self.map[c].items())) + "}" for c in sorted(self.map))
+        return "(true,{" + comps + "})"
+
+
+def edge_to_candidate(v1, v2):  # BipartitenessCheck.java:54-61
+    src, trg = min(v1, v2), max(v1, v2)
+    c = PyCandidates(True)
+    c.add(src, src, True)
+    c.add(src, trg, False)  # a self loop: add returns false, ignored (:58-59)
+    return c
+
+
+def run_stream(pairs, starts, partitions=1):
+    """Per window: the Merger's summary after folding the window's partitions and combining them."""
+    summary = PyCandidates(True)
+    out = []
+    for w in range(len(starts) - 1):
+        b, e = int(starts[w]), int(starts[w + 1])
+        if e == b:
+            out.append(None)
+            continue
+        acc = None
+        for p in range(partitions):
+            pb, pe = b + (e - b) * p // partitions, b + (e - b) * (p + 1) // partitions
+            if pe == pb:
+                continue
+            part = PyCandidates(True)
+            for u, v in pairs[pb:pe]:
+                part = part.merge(edge_to_candidate(int(u), int(v)))  # updateFunction.foldEdges
+            acc = part if acc is None else acc.merge(part)          # combineFunction.reduce
+        summary = acc.merge(summary)                                 # Merger: combine.reduce(window, summary)
+        out.append(summary)
+    return out
+
+
+def canonical(c, V):
+    """success + canonical words: (component min << 1) | (sign differs from the min's sign)."""
+    words = [UNSEEN] * V
+    if c.success:
+        for comp in c.map.values():
+            m = min(comp)
+            for v, s in comp.items():
+                words[v] = (m << 1) | (0 if s == comp[m] else 1)
+    return c.success, words
+
+
+def truth(pairs_so_far, V):
+    """networkx: bipartite iff no odd cycle among non-loop edges; components with 2-colourings."""
+    g = nx.Graph()
+    for u, v in pairs_so_far:
+        g.add_node(int(u))
+        g.add_node(int(v))
+        if u != v:
+            g.add_edge(int(u), int(v))
+    ok = nx.is_bipartite(g)
+    words = [UNSEEN] * V
+    if ok:
+        for comp in nx.connected_components(g):
+            m = min(comp)
+            col = nx.bipartite.color(g.subgraph(comp))
+            for v in comp:
+                words[v] = (m << 1) | (col[v] ^ col[m])
+    return ok, words
+
+
+def literal_is_partition(c):
+    """Whether the literal restatement's components are disjoint (see the module note on Candidates.java:176-189)."""
+    seen = set()
+    for comp in c.map.values():
+        if seen & set(comp):
+            return False
+        seen |= set(comp)
+    return True
+
+
+def stream_fixture(name, pairs, starts, V, partitions=1, note=""):
+    """Windows pinned by networkx (the intended semantics); the literal restatement of the reference is run
+    alongside and its agreement recorded per window."""
+    res = run_stream(pairs, starts, partitions)
+    windows = []
+    for w, c in enumerate(res):
+        if c is None:
+            windows.append(None)
+            continue
+        t_ok, t_words = truth(pairs[: int(starts[w + 1])], V)
+        ok, words = canonical(c, V)
+        agrees = (ok == t_ok) and (not ok or (literal_is_partition(c) and words == t_words))
+        windows.append({"success": t_ok, "words": t_words, "reference_literal_agrees": agrees})
+    fx = {"name": name, "V": V, "partitions": partitions, "pairs": [[int(u), int(v)] for u, v in pairs],
+          "window_starts": [int(s) for s in starts], "windows": windows, "note": note}
+    with open(os.path.join(HERE, f"bip_{name}.json"), "w") as f:
+        json.dump(fx, f, separators=(",", ":"))
+    print(name, len(pairs), "edges", len(starts) - 1, "windows; success:",
+          [w["success"] if w else None for w in windows], "literal agrees:",
+          [w["reference_literal_agrees"] if w else None for w in windows])
+
+
+def main():
+    # 2. the reference's KATs (processing-time windows of 500 ms over 6 edges at parallelism 1: one window)
+    kat_b = [[1, 2], [1, 3], [1, 4], [4, 5], [4, 7], [4, 9]]
+    kat_n = [[1, 2], [2, 3], [3, 1], [4, 5], [5, 7], [4, 1]]
+    res_b = run_stream(np.array(kat_b), [0, 6])[0]
+    res_n = run_stream(np.array(kat_n), [0, 6])[0]
+    expect_b = "(true,{1={1=(1,true), 2=(2,false), 3=(3,false), 4=(4,false), 5=(5,true), 7=(7,true), 9=(9,true)}})"
+    assert res_b.to_string() == expect_b, res_b.to_string()
+    assert res_n.to_string() == "(false,{})", res_n.to_string()
+    with open(os.path.join(HERE, "bip_kat.json"), "w") as f:
+        json.dump({"bipartite": {"edges": kat_b, "expected": expect_b, "V": 10, "words": canonical(res_b, 10)[1],
+                                 "source": "src/test/java/org/apache/flink/graph/streaming/example/test/"
+                                           "BipartitenessCheckTest.java:18-19, :26-35"},
+                   "non_bipartite": {"edges": kat_n, "expected": "(false,{})", "V": 10,
+                                     "source": "…/example/test/NonBipartitnessCheckTest.java:18-19, :26-35"}},
+                  f, indent=1)
+    print("KATs ok")
+    rng = np.random.default_rng(20261016)
+    # 3. random bipartite streams: edges only between the two halves of a random 2-colouring
+    V = 48
+    side = rng.integers(0, 2, V)
+    A, B = np.flatnonzero(side == 0), np.flatnonzero(side == 1)
+    e = np.stack([rng.choice(A, 90), rng.choice(B, 90)], axis=1)
+    flip = rng.integers(0, 2, 90).astype(bool)
+    e[flip] = e[flip][:, ::-1]
+    stream_fixture("random_bipartite", e, [0, 20, 21, 55, 90], V, partitions=1)
+    stream_fixture("random_bipartite_p3", e, [0, 20, 21, 55, 90], V, partitions=3)
+    # a bipartite stream whose last window closes an odd cycle (success flips to false)
+    e2 = np.concatenate([e[:60], [[int(A[0]), int(A[1])]], e[60:70]])  # two vertices of one side: odd cycle once
+    stream_fixture("closes_odd_cycle", e2, [0, 30, 61, 71], V, partitions=1)
+    # self loops and duplicates: only add the vertex (reference behaviour)
+    e3 = np.array([[5, 5], [5, 6], [6, 6], [7, 8], [8, 7], [5, 6], [9, 9]])
+    stream_fixture("self_loops", e3, [0, 3, 7], 12, partitions=1)
+    # larger: many components, two windows, 4 partitions (the combine path); bipartite throughout
+    V = 2000
+    side = rng.integers(0, 2, V)
+    A, B = np.flatnonzero(side == 0), np.flatnonzero(side == 1)
+    e4 = np.stack([rng.choice(A, 1500), rng.choice(B, 1500)], axis=1)
+    stream_fixture("large_bipartite_p4", e4, [0, 700, 1500], V, partitions=4)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,68 @@
+"""CPU: pin the BipartitenessCheck oracle (oracle/bip_oracle.c) against the golden fixtures.
+
+tests/golden/bip_kat.json holds the reference's own tests (BipartitenessCheckTest / NonBipartitnessCheckTest);
+tests/golden/bip_*.json the streams pinned by networkx (tests/golden/make_golden_bip.py, which also records where a
+literal restatement of the reference's Candidates.merge diverges from the intended partition semantics).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle as orc
+
+UNSEEN = 0xFFFFFFFF
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def canonical_string(success, words):
+    """Candidates.toString of the canonical summary (the minimum vertex of each component carries `true`)."""
+    if not success:
+        return "(false,{})"
+    comps = {}
+    for v in np.flatnonzero(words != UNSEEN).tolist():
+        comps.setdefault(int(words[v]) >> 1, []).append((v, (int(words[v]) & 1) == 0))
+    body = ", ".join(f"{c}={{" + ", ".join(f"{v}=({v},{'true' if s else 'false'})" for v, s in sorted(m)) + "}"
+                     for c, m in sorted(comps.items()))
+    return "(true,{" + body + "})"
+
+
+def test_oracle_reference_kats(golden):
+    fx = golden("bip_kat.json")
+    b = fx["bipartite"]
+    r = orc.bip_stream(np.array(b["edges"], dtype=np.uint32), [0, len(b["edges"])], b["V"])
+    assert r["success"][0]
+    assert r["words"][0].tolist() == b["words"]
+    assert canonical_string(True, r["words"][0]) == b["expected"]  # the reference test's expected line
+    n = fx["non_bipartite"]
+    r = orc.bip_stream(np.array(n["edges"], dtype=np.uint32), [0, len(n["edges"])], n["V"])
+    assert not r["success"][0]
+    assert canonical_string(False, r["words"][0]) == n["expected"]
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(HERE, "golden", "bip_*.json"))))
+def test_oracle_streams(path, golden):
+    name = os.path.basename(path)
+    if name == "bip_kat.json":
+        return
+    fx = golden(name)
+    pairs = np.array(fx["pairs"], dtype=np.uint32)
+    r = orc.bip_stream(pairs, fx["window_starts"], fx["V"], partitions=fx["partitions"])
+    for w, want in enumerate(fx["windows"]):
+        assert bool(r["emitted"][w]) == (want is not None)
+        if want is None:
+            continue
+        assert bool(r["success"][w]) == want["success"], (name, w)
+        if want["success"]:
+            assert r["words"][w].tolist() == want["words"], (name, w)
+
+
+def test_oracle_partitions_do_not_change_the_result(golden):
+    """The combine topology (partitions per window) never changes the canonical summary."""
+    fx = golden("bip_large_bipartite_p4.json")
+    pairs = np.array(fx["pairs"], dtype=np.uint32)
+    ref = orc.bip_stream(pairs, fx["window_starts"], fx["V"], partitions=1)
+    for p in (2, 3, 7):
+        r = orc.bip_stream(pairs, fx["window_starts"], fx["V"], partitions=p)
+        assert np.array_equal(r["words"], ref["words"]) and np.array_equal(r["success"], ref["success"])

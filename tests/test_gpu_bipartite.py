@@ -1,0 +1,129 @@
+"""GPU: BipartitenessCheck's signed forest (csrc/gelly_bip.hip, gcc_signed_*) and ConnectedComponentsTree's
+pairwise combine, through the C ABI, against the reference's KATs, the golden fixtures and the CPU oracle.
+
+Parity contract: per window, the success flag and per vertex the canonical word
+(component min << 1) | (sign differs from the min's); the reference KATs' toString lines verbatim.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from gelly_stream import (BipartitenessCheck, Candidates, ConnectedComponents, ConnectedComponentsTree,
+                          SimpleEdgeStream)
+from gelly_stream import generators as G
+
+pytestmark = pytest.mark.gpu
+UNSEEN = 0xFFFFFFFF
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_reference_kats_verbatim(golden):
+    """BipartitenessCheckTest / NonBipartitnessCheckTest: the emitted line, character for character."""
+    fx = golden("bip_kat.json")
+    for key in ("bipartite", "non_bipartite"):
+        k = fx[key]
+        stream = SimpleEdgeStream(np.array(k["edges"], dtype=np.uint32))
+        out = [c.toString() for c in stream.aggregate(BipartitenessCheck(500, id_capacity=k["V"]))]
+        assert out == [k["expected"]], key
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(HERE, "golden", "bip_*.json"))))
+def test_fixture_streams(path, golden):
+    name = os.path.basename(path)
+    if name == "bip_kat.json":
+        return
+    fx = golden(name)
+    pairs = np.array(fx["pairs"], dtype=np.uint32)
+    starts = fx["window_starts"]
+    c = Candidates(fx["V"])
+    for w, want in enumerate(fx["windows"]):
+        c.fold(pairs[starts[w]:starts[w + 1]])
+        if want is None:
+            continue
+        assert c.getSuccess() == want["success"], (name, w)
+        if want["success"]:
+            assert c.words().tolist() == want["words"], (name, w)
+        else:
+            assert c.getMap() == {} and c.toString() == "(false,{})"
+    c.close()
+
+
+def bipartite_stream(n_ids, n_edges, seed, odd_edge_at=None):
+    rng = np.random.default_rng(seed)
+    side = rng.integers(0, 2, n_ids)
+    A, B = np.flatnonzero(side == 0), np.flatnonzero(side == 1)
+    e = np.stack([rng.choice(A, n_edges), rng.choice(B, n_edges)], axis=1).astype(np.uint32)
+    flip = rng.integers(0, 2, n_edges).astype(bool)
+    e[flip] = e[flip][:, ::-1]
+    if odd_edge_at is not None:  # one edge inside side A closes an odd cycle (once both ends are connected)
+        e[odd_edge_at] = [A[0], A[1]]
+    return e
+
+
+@pytest.mark.parametrize("odd", [False, True])
+def test_large_random_vs_oracle(odd):
+    """1M edges over 256K ids in 4 windows, device-resident, vs the oracle every window."""
+    V, E = 1 << 18, 1 << 20
+    pairs = bipartite_stream(V, E, 11, odd_edge_at=(3 * E // 4) if odd else None)
+    starts = [0, 1000, E // 2, 3 * E // 4 + 1, E]
+    want = orc.bip_stream(pairs, starts, V, partitions=3)
+    import torch
+
+    d = torch.from_numpy(pairs.view(np.int32)).cuda()
+    c = Candidates(V)
+    for w in range(len(starts) - 1):
+        c.fold_device(d.data_ptr() + 8 * starts[w], starts[w + 1] - starts[w])
+        assert c.getSuccess() == bool(want["success"][w]), w
+        if want["success"][w]:
+            assert np.array_equal(c.words(), want["words"][w]), w
+    c.close()
+
+
+def test_merge_is_combine_function():
+    """combineFunction.reduce(c1, c2) = c1.merge(c2): two partials merged equal one fold of both halves; a
+    failed input fails the result (Candidates.merge :78-81)."""
+    V, E = 1 << 14, 1 << 16
+    pairs = bipartite_stream(V, E, 5)
+    a, b, whole = Candidates(V), Candidates(V), Candidates(V)
+    a.fold(pairs[: E // 3])
+    b.fold(pairs[E // 3:])
+    whole.fold(pairs)
+    assert a.merge(b) is a
+    assert a.getSuccess() and np.array_equal(a.words(), whole.words())
+    bad = Candidates(V)
+    bad.fold(np.array([[1, 2], [2, 3], [3, 1]], dtype=np.uint32))
+    assert not bad.getSuccess()
+    assert not a.merge(bad).getSuccess() and a.toString() == "(false,{})"
+    for x in (a, b, whole, bad):
+        x.close()
+
+
+def test_self_loops_only_add_the_vertex():
+    c = Candidates(16)
+    c.fold(np.array([[5, 5], [7, 7], [7, 8]], dtype=np.uint32))
+    assert c.getSuccess()
+    assert c.toString() == "(true,{5={5=(5,true)}, 7={7=(7,true), 8=(8,false)}})"
+    c.close()
+
+
+def test_connected_components_tree_matches_bulk():
+    """ConnectedComponentsTree (SummaryTreeReduce's pairwise combine of 8 partial forests per window) emits the
+    same partition as ConnectedComponents and the oracle, every window."""
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=14, n_edges=1 << 18)
+    pairs = G.generate_host(cfg)
+    _, V = cfg.info()
+    W = 1 << 16
+    starts = np.arange(0, len(pairs) + 1, W, dtype=np.uint64)
+    want = orc.cc_stream(pairs, starts, V, partitions=8, want_labels=True)["labels"]
+    tree = SimpleEdgeStream(pairs, edges_per_window=W, parallelism=8).aggregate(
+        ConnectedComponentsTree(1000, id_capacity=V, degree=8))
+    bulk = SimpleEdgeStream(pairs, edges_per_window=W).aggregate(ConnectedComponents(1000, id_capacity=V))
+    n = 0
+    for w, (t, b) in enumerate(zip(tree, bulk)):
+        assert np.array_equal(t.labels(), want[w]), w
+        assert np.array_equal(b.labels(), want[w]), w
+        n += 1
+    assert n == len(starts) - 1

@@ -16,8 +16,10 @@ from gelly_stream import generators as G  # noqa: E402
 
 CONFIGS = [
     ("default", {}),
-    ("nopipe", {"pipe": 0}),
+    ("nohook", {"hook": 0}),
     ("depth8", {"depth": 8}),
+    ("sdiv16", {"sample_div": 16}),
+    ("nofilter", {"filter": 0}),
 ]
 
 
