@@ -442,6 +442,7 @@ constexpr u64 kHubSample = 2048;  // edges sampled for the hub vote (2 per threa
 
 __device__ __forceinline__ void hub_count(u32 x, u32* s_key, u32* s_cnt) {
     u32 s = (u32)(gcc_splitmix64(x) & (kHubSlots - 1));
+#pragma unroll 1
     for (u32 p = 0; p < kHubProbe; ++p, s = (s + 1) & (kHubSlots - 1)) {
         const u32 k = atomicCAS(&s_key[s], UNSEEN, x);
         if (k == UNSEEN || k == x) {
@@ -453,14 +454,12 @@ __device__ __forceinline__ void hub_count(u32 x, u32* s_key, u32* s_cnt) {
 
 __device__ __forceinline__ bool hub_better(u32 c, u32 k, u32 bc, u32 bk) { return c > bc || (c == bc && c && k < bk); }
 
-// Elects h and initialises C = {h}: flags (zeroed up to a whole bitmap word) and the bitmap. Every block of
-// the grid elects the same h (deterministic argmax) and clears its own share of both arrays.
-__global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restrict__ edges, u64 n_sample,
-                                                             u8* __restrict__ flags, u32* __restrict__ bits32, u32 n,
-                                                             u32* __restrict__ gmin) {
-    extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
-    u32* s_key = s_dyn;
-    u32* s_cnt = s_dyn + kHubSlots;
+// The hub election of one 1024-thread block: h = the most frequent endpoint of the first n_sample (<= 2048)
+// edges, ties to the smaller id — deterministic, so every block that runs it elects the same h. s_tab: 2 x
+// kHubSlots u32 of LDS (free again on return). Every thread returns h.
+__device__ __forceinline__ u32 hub_elect(const u64* __restrict__ edges, u64 n_sample, u32* s_tab) {
+    u32* s_key = s_tab;
+    u32* s_cnt = s_tab + kHubSlots;
     __shared__ u32 s_bc[kHubBlock / 64], s_bk[kHubBlock / 64];
     constexpr int kPer = (int)(kHubSample / kHubBlock);
     u64 e[kPer];
@@ -469,9 +468,12 @@ __global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restri
         const u64 i = threadIdx.x + (u64)k * kHubBlock;
         e[k] = i < n_sample ? edges[i] : ~0ull;
     }
-    for (u32 s = threadIdx.x; s < kHubSlots; s += kHubBlock) {
-        s_key[s] = UNSEEN;
-        s_cnt[s] = 0;
+    {
+        const u32x4 kz = {UNSEEN, UNSEEN, UNSEEN, UNSEEN}, cz = {0, 0, 0, 0};
+        for (u32 s = threadIdx.x; s < kHubSlots / 4; s += kHubBlock) {
+            reinterpret_cast<u32x4*>(s_key)[s] = kz;
+            reinterpret_cast<u32x4*>(s_cnt)[s] = cz;
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -508,7 +510,16 @@ __global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restri
             }
     }
     __syncthreads();
-    const u32 h = s_bk[0];  // n_sample >= 1, so some endpoint was counted
+    return s_bk[0];  // n_sample >= 1, so some endpoint was counted
+}
+
+// Elects h and initialises C = {h}: flags (zeroed up to a whole bitmap word) and the bitmap. Every block of
+// the grid elects the same h (deterministic argmax) and clears its own share of both arrays.
+__global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restrict__ edges, u64 n_sample,
+                                                             u8* __restrict__ flags, u32* __restrict__ bits32, u32 n,
+                                                             u32* __restrict__ gmin) {
+    extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
+    const u32 h = hub_elect(edges, n_sample, s_dyn);
     // this block's share: 32 ids per unit = 32 flag bytes (two 16-B stores) + one bitmap word
     const u64 nu = ((u64)n + 31) / 32;
     const u64 per = (nu + gridDim.x - 1) / gridDim.x;
@@ -533,10 +544,14 @@ __global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restri
 // One BFS pass over the prefix. LDS = true: every block (one per CU) holds the bitmap of C as of the last
 // pack in LDS; a discovered id is set there too (LDS atomicOr: propagation inside the block, and each id is
 // flagged once per block), then flagged in HBM. LDS = false: lookups go to the global bitmap.
-template <bool LDS, int BLOCK, bool NT>
+// HUB (first pass of the fused seeding, LDS only): there is no C yet — the block elects h itself (hub_elect,
+// the same h in every block), starts from the LDS bitmap {h} instead of copying one in, and block 0 flags h.
+// Flags hold the seeding's epoch (1..255) instead of 1, so no pass ever has to clear them.
+template <bool LDS, int BLOCK, bool NT, bool HUB>
 __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__ edges, u64 n,
                                                          const u32* __restrict__ bits32, u32 nwords32,
-                                                         u8* __restrict__ flags, u32* __restrict__ gmin) {
+                                                         u8* __restrict__ flags, u32* __restrict__ gmin, u8 epoch) {
+    static_assert(!HUB || (LDS && BLOCK == kHubBlock), "the fused hub election needs the LDS variant");
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     __shared__ u32 s_min;
     constexpr int D = 8;  // 16-B edge pairs in flight per lane
@@ -557,14 +572,27 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
         if ((u64)k < cnt) q[k] = ld(body + i + k * stride);
     u32* bm = const_cast<u32*>(bits32);
     if (threadIdx.x == 0) s_min = UNSEEN;
-    if constexpr (LDS) {
+    u32 lmin = UNSEEN;
+    if constexpr (HUB) {
+        const u32 h = hub_elect(edges, n < kHubSample ? n : kHubSample, s_dyn);  // ends with a barrier
+        const u32x4 z = {0, 0, 0, 0};
+        for (u32 w = threadIdx.x; w < nwords32 / 4; w += BLOCK) reinterpret_cast<u32x4*>(s_dyn)[w] = z;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            s_dyn[h >> 5] = 1u << (h & 31);
+            if (blockIdx.x == 0) {
+                flags[h] = epoch;
+                lmin = h;
+            }
+        }
+        bm = s_dyn;
+    } else if constexpr (LDS) {
         const u32x4* src = reinterpret_cast<const u32x4*>(bits32);
         u32x4* dst = reinterpret_cast<u32x4*>(s_dyn);
         for (u32 w = threadIdx.x; w < nwords32 / 4; w += BLOCK) dst[w] = src[w];
         bm = s_dyn;
     }
     __syncthreads();
-    u32 lmin = UNSEEN;
     auto visit = [&](u32 a, u32 b) {
         const u32 ia = (bm[a >> 5] >> (a & 31)) & 1u, ib = (bm[b >> 5] >> (b & 31)) & 1u;
         if (ia != ib) {
@@ -572,7 +600,7 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
             bool fresh = true;
             if constexpr (LDS) fresh = !(atomicOr(&bm[x >> 5], m) & m);
             if (fresh) {
-                flags[x] = 1;
+                flags[x] = epoch;
                 lmin = min(lmin, x);
             }
         }
@@ -606,15 +634,21 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
 // Pack the flag bytes into the bitmap of C (8 lanes = one u32 word, 4 ids per lane). PARENT = true (the
 // last step of the seeding): also parent[v] = (v in C) ? gmin : UNSEEN with 16-B stores, and publish gmin as
 // the tracked component.
+// A flag byte marks C iff it equals the seeding's epoch. PARENT also re-arms gmin_next (the other gmin slot,
+// which the next seeding's atomicMins start from).
 template <bool PARENT>
 __global__ __launch_bounds__(kBlock) void seed_pack_kernel(u32* __restrict__ parent, u32 n, const u8* __restrict__ flags,
                                                            u32* __restrict__ bits32, const u32* __restrict__ gmin,
-                                                           u32* __restrict__ giant) {
+                                                           u32* __restrict__ giant, u8 epoch, u32* __restrict__ gmin_next) {
     u32 g = 0;
     if constexpr (PARENT) {
         g = *gmin;
-        if (blockIdx.x == 0 && threadIdx.x == 0) *giant = g;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            *giant = g;
+            if (gmin_next) *gmin_next = UNSEEN;
+        }
     }
+    const u32 ep4 = 0x01010101u * epoch;
     const u64 stride = (u64)gridDim.x * kBlock;
     const u64 nq = ((u64)n + 31) / 32 * 8;  // whole bitmap words
     const u32* f32 = reinterpret_cast<const u32*>(flags);
@@ -624,8 +658,9 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(u32* __restrict__ par
         const u64 q = q0 + lane;
         u32 nib = 0;
         if (q < nq) {
-            const u32 f = f32[q];  // flag bytes of ids 4q..4q+3 (0 or 1 each)
-            nib = (f & 1u) | ((f >> 7) & 2u) | ((f >> 14) & 4u) | ((f >> 21) & 8u);
+            const u32 f = f32[q] ^ ep4;  // flag bytes of ids 4q..4q+3: 0 iff in C
+            nib = ((f & 0xFFu) == 0) | (((f & 0xFF00u) == 0) << 1) | (((f & 0xFF0000u) == 0) << 2) |
+                  (((f & 0xFF000000u) == 0) << 3);
             if constexpr (PARENT) {
                 const u64 v = 4 * q;
                 if (v + 3 < n) {
@@ -872,13 +907,14 @@ struct FoldTune {
     // seeded fold of a fresh forest (seed_* kernels): BFS from a hub over the first 1/seed_div of the batch
     bool seed = true;
     int seed_passes = 2;
-    u64 seed_div = 2;
-    u64 seed_div1 = 2;  // the first BFS pass covers 1/seed_div1 of the batch (>= 1/seed_div)
+    u64 seed_div = 3;
+    u64 seed_div1 = 3;  // the first BFS pass covers 1/seed_div1 of the batch (>= 1/seed_div)
     double seed_refresh = 0;  // refresh point of a seeded batch (fraction; 0 = none)
     bool hook = true;  // direct atomicMin hook of (T, new id) edges in the filtered stream (filter_round)
     u32 drain_at = 64;  // a wave drains its slow-edge ring once this many edges are pending (1..64)
     bool seed_nt = true;  // non-temporal loads in the BFS passes (false: the prefix may stay in the MALL)
     bool seed_global = false;  // also seed when the bitmap does not fit LDS (global-bitmap BFS lookups)
+    bool seed_fuse = true;  // the first BFS pass elects the hub itself (no seed_hub launch, no flag clearing)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -904,6 +940,11 @@ struct gcc_forest {
     bool has_giant = false;
     int giant_slot = 0;  // d_giant[giant_slot] = root of the tracked component as of the last refresh
     u32* d_qcount = nullptr;  // per-block slow-edge counts of the last filtered launch (measurement)
+    // fused seeding: dedicated flag bytes (one per id, rounded up to a bitmap word), marked with an epoch
+    // 1..255 so they need clearing once per 255 seedings; gmin slot d_giant[2 + seeds % 2]
+    u8* d_flags = nullptr;
+    u32 flag_epoch = 0;  // the last epoch written into d_flags (0: needs clearing)
+    u64 seeds = 0;
 
     // pinned double-buffered staging for host-fed edges (per-edge foldEdges appends here)
     static constexpr u64 kStageEdges = 1ull << 20;  // 8 MiB per slot
@@ -1001,6 +1042,7 @@ static int alloc_filter(gcc_forest* h) {
     if (h->d_bits) return GCC_OK;
     HIP_TRY(hipMalloc((void**)&h->d_bits, (size_t)h->nwords() * sizeof(u64) + 16));
     HIP_TRY(hipMalloc((void**)&h->d_giant, 4 * sizeof(u32)));
+    HIP_TRY(hipMemsetAsync(h->d_giant, 0xFF, 4 * sizeof(u32), h->stream));  // both gmin slots start at UNSEEN
     return GCC_OK;
 }
 
@@ -1103,57 +1145,83 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
     int rc = alloc_filter(h);
     if (rc) return rc;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
-    u8* flags = reinterpret_cast<u8*>(h->d_spare);  // free until the next compress: one flag byte per id
     u32* bits = reinterpret_cast<u32*>(h->d_bits);
-    u32* gmin = h->d_giant + 2;
-    const unsigned hub_grid = (unsigned)std::max<u64>(1, std::min<u64>((u64)h->n_cu, (u64)h->cap >> 16));
-    static bool hub_attr = false;
-    if (!hub_attr) {
-        HIP_TRY(hipFuncSetAttribute((const void*)seed_hub_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)(2 * kHubSlots * sizeof(u32))));
-        hub_attr = true;
+    const u32 nw32 = 2 * (h->nwords() + (h->nwords() & 1));  // u32 bitmap words, rounded to 16 B
+    const bool lds = nw32 / 2 <= kLdsBitmapMaxWords;
+    const bool fuse = t.seed_fuse && lds && t.seed_passes > 0;
+    // gmin slot of this seeding (re-armed to UNSEEN by the previous seeding's last pack, or at allocation)
+    const u64 seed_no = h->seeds++;
+    u32* gmin = h->d_giant + 2 + (seed_no & 1);
+    u32* gmin_next = h->d_giant + 2 + ((seed_no + 1) & 1);
+    u8* flags;
+    u8 epoch = 1;
+    if (fuse) {  // dedicated epoch-marked flags: nothing to clear
+        const size_t flag_bytes = (size_t)nw32 * 32;  // one byte per id of every bitmap word
+        if (!h->d_flags) {
+            HIP_TRY(hipMalloc((void**)&h->d_flags, flag_bytes));
+            h->flag_epoch = 0;
+        }
+        if (h->flag_epoch == 0 || h->flag_epoch == 255) {
+            HIP_TRY(hipMemsetAsync(h->d_flags, 0, flag_bytes, h->stream));
+            h->flag_epoch = 0;
+        }
+        epoch = (u8)++h->flag_epoch;
+        flags = h->d_flags;
+    } else {
+        flags = reinterpret_cast<u8*>(h->d_spare);  // free until the next compress: one flag byte per id
+        const unsigned hub_grid = (unsigned)std::max<u64>(1, std::min<u64>((u64)h->n_cu, (u64)h->cap >> 16));
+        static bool hub_attr = false;
+        if (!hub_attr) {
+            HIP_TRY(hipFuncSetAttribute((const void*)seed_hub_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(2 * kHubSlots * sizeof(u32))));
+            hub_attr = true;
+        }
+        rc = launch_k(h, "seed_hub", 0, seed_hub_kernel, dim3(hub_grid), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32),
+                      edges, std::min(n, kHubSample), flags, bits, h->cap, gmin);
+        if (rc) return rc;
     }
-    rc = launch_k(h, "seed_hub", 0, seed_hub_kernel, dim3(hub_grid), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32), edges,
-                  std::min(n, kHubSample), flags, bits, h->cap, gmin);
-    if (rc) return rc;
     const u64 pref = std::min(n, std::max<u64>(t.filter_min_batch, n / std::max<u64>(1, t.seed_div)));
     // the first pass only has to reach the hubs next to h: a shorter prefix
     const u64 pref1 = std::min(pref, std::max<u64>(t.filter_min_batch, n / std::max<u64>(1, t.seed_div1)));
-    const u32 nw32 = 2 * (h->nwords() + (h->nwords() & 1));  // u32 bitmap words, rounded to 16 B
-    const bool lds = nw32 / 2 <= kLdsBitmapMaxWords;
     const unsigned pack_grid = grid_for(((u64)h->cap + 3) / 4, kMaxGrid);
     for (int p = 0; p < t.seed_passes; ++p) {
         const u64 np = p == 0 ? pref1 : pref;
         if (lds) {
             static bool attr = false;
             if (!attr) {
-                for (const void* f : {(const void*)seed_bfs_kernel<true, kFilterBlockLds, true>,
-                                      (const void*)seed_bfs_kernel<true, kFilterBlockLds, false>})
+                for (const void* f : {(const void*)seed_bfs_kernel<true, kFilterBlockLds, true, false>,
+                                      (const void*)seed_bfs_kernel<true, kFilterBlockLds, false, false>,
+                                      (const void*)seed_bfs_kernel<true, kFilterBlockLds, true, true>,
+                                      (const void*)seed_bfs_kernel<true, kFilterBlockLds, false, true>})
                     HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                 (int)(kLdsBitmapMaxWords * sizeof(u64))));
                 attr = true;
             }
-            const size_t sh = (size_t)nw32 * sizeof(u32);
-            rc = t.seed_nt ? launch_k(h, "seed_bfs", np, seed_bfs_kernel<true, kFilterBlockLds, true>, dim3(h->n_cu),
-                                      dim3(kFilterBlockLds), sh, edges, np, (const u32*)bits, nw32, flags, gmin)
-                           : launch_k(h, "seed_bfs", np, seed_bfs_kernel<true, kFilterBlockLds, false>, dim3(h->n_cu),
-                                      dim3(kFilterBlockLds), sh, edges, np, (const u32*)bits, nw32, flags, gmin);
+            const bool hub = fuse && p == 0;
+            // the fused first pass also holds the election's hash table (2 x kHubSlots u32) in the same LDS
+            const size_t sh = std::max<size_t>((size_t)nw32 * sizeof(u32), hub ? 2 * kHubSlots * sizeof(u32) : 0);
+#define GCC_BFS(NT, HUB)                                                                                       \
+    launch_k(h, "seed_bfs", np, seed_bfs_kernel<true, kFilterBlockLds, NT, HUB>, dim3(h->n_cu), dim3(kFilterBlockLds), \
+             sh, edges, np, (const u32*)bits, nw32, flags, gmin, epoch)
+            rc = t.seed_nt ? (hub ? GCC_BFS(true, true) : GCC_BFS(true, false))
+                           : (hub ? GCC_BFS(false, true) : GCC_BFS(false, false));
+#undef GCC_BFS
         } else {
             const unsigned grid = grid_for((np + 1) / 2, kMaxGrid);
-            rc = t.seed_nt ? launch_k(h, "seed_bfs", np, seed_bfs_kernel<false, kBlock, true>, dim3(grid), dim3(kBlock), 0,
-                                      edges, np, (const u32*)bits, nw32, flags, gmin)
-                           : launch_k(h, "seed_bfs", np, seed_bfs_kernel<false, kBlock, false>, dim3(grid), dim3(kBlock), 0,
-                                      edges, np, (const u32*)bits, nw32, flags, gmin);
+            rc = t.seed_nt ? launch_k(h, "seed_bfs", np, seed_bfs_kernel<false, kBlock, true, false>, dim3(grid),
+                                      dim3(kBlock), 0, edges, np, (const u32*)bits, nw32, flags, gmin, epoch)
+                           : launch_k(h, "seed_bfs", np, seed_bfs_kernel<false, kBlock, false, false>, dim3(grid),
+                                      dim3(kBlock), 0, edges, np, (const u32*)bits, nw32, flags, gmin, epoch);
         }
         if (rc) return rc;
         if (p + 1 < t.seed_passes) {
             rc = launch_k(h, "seed_pack", 0, seed_pack_kernel<false>, dim3(pack_grid), dim3(kBlock), 0, h->d_parent, h->cap,
-                          (const u8*)flags, bits, (const u32*)gmin, h->d_giant + h->giant_slot);
+                          (const u8*)flags, bits, (const u32*)gmin, h->d_giant + h->giant_slot, epoch, (u32*)nullptr);
             if (rc) return rc;
         }
     }
     rc = launch_k(h, "seed_init", 0, seed_pack_kernel<true>, dim3(pack_grid), dim3(kBlock), 0, h->d_parent, h->cap,
-                  (const u8*)flags, bits, (const u32*)gmin, h->d_giant + h->giant_slot);
+                  (const u8*)flags, bits, (const u32*)gmin, h->d_giant + h->giant_slot, epoch, gmin_next);
     if (rc) return rc;
     h->pending_reset = false;
     h->has_giant = true;
@@ -1417,6 +1485,7 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (h->d_witness) (void)hipFree(h->d_witness);
     if (h->d_bits) (void)hipFree(h->d_bits);
     if (h->d_giant) (void)hipFree(h->d_giant);
+    if (h->d_flags) (void)hipFree(h->d_flags);
     if (h->d_qcount) (void)hipFree(h->d_qcount);
     if (h->d_counts) (void)hipFree(h->d_counts);
     for (auto& pe : h->kev) {
@@ -1776,6 +1845,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "seed_div") t.seed_div = std::max<u64>(1, (u64)value);
     else if (k == "seed_div1") t.seed_div1 = std::max<u64>(1, (u64)value);
     else if (k == "seed_refresh") t.seed_refresh = value;
+    else if (k == "seed_fuse") t.seed_fuse = value != 0;
     else return set_err(GCC_E_INVALID, "unknown tuning key '%s'", key);
     return GCC_OK;
 }

@@ -27,8 +27,11 @@ def main():
     global CONFIGS
     wl = sys.argv[1] if len(sys.argv) > 1 else "c2_rmat20"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 7
-    if len(sys.argv) > 3:  # only the named configs
-        CONFIGS = [c for c in CONFIGS if c[0] in sys.argv[3].split(",")]
+    if len(sys.argv) > 3:  # only the named configs, or a JSON object {name: {knob: value}}
+        if sys.argv[3].startswith("{"):
+            CONFIGS = list(json.loads(sys.argv[3]).items())
+        else:
+            CONFIGS = [c for c in CONFIGS if c[0] in sys.argv[3].split(",")]
     cfg = G.CONFIGS[wl]
     E, V = cfg.info()
     d = torch.empty(2 * E, dtype=torch.int32, device="cuda:0")
