@@ -168,10 +168,15 @@ __device__ __forceinline__ void filter_round(const bool* valid, const u32* a, co
                                              HookCarry<N>& carry) {
     HookCarry<N> cur;
     bool slow[N];
-    u32 pa[N], pb[N];
+    u32 pa[N], pb[N], wa[N], wb[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {  // every bitmap lookup of the round first: one LDS wait, not one per edge
+        wa[k] = bm[a[k] >> 5];
+        wb[k] = bm[b[k] >> 5];
+    }
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-        const u32 ia = in_c<LDS>(bm, a[k]), ib = in_c<LDS>(bm, b[k]);
+        const u32 ia = (wa[k] >> (a[k] & 31)) & 1u, ib = (wb[k] >> (b[k] & 31)) & 1u;
         cur.other[k] = ia ? b[k] : a[k];
         cur.hook[k] = valid[k] && (ia ^ ib) && cur.other[k] > g;
         slow[k] = valid[k] && !(ia & ib) && !cur.hook[k];
@@ -233,10 +238,14 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
             while (true) {
                 const u64 nb = base + DEPTH * stride;
                 const bool more = nb + 63 + (DEPTH - 1) * stride < n2;  // wave-uniform
+                // issued unconditionally (clamped in range; the last, unused round re-reads a valid pair): a load
+                // under a branch leaves the compiler unable to count it, and its s_waitcnt then drains the whole
+                // queue, prefetch included, before the current round is filtered
                 u32x4 nq[DEPTH];
-                if (more) {
 #pragma unroll
-                    for (int k = 0; k < DEPTH; ++k) nq[k] = __builtin_nontemporal_load(body + nb + lane + k * stride);
+                for (int k = 0; k < DEPTH; ++k) {
+                    const u64 j = nb + lane + k * stride;
+                    nq[k] = __builtin_nontemporal_load(body + (j < n2 ? j : n2 - 1));
                 }
                 if constexpr (HOOK) {
                     bool vv[2 * DEPTH];
@@ -430,15 +439,15 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
 //      y ∈ C — a BFS from h over the prefix edges, on one flag byte per id. Setting a flag is an idempotent
 //      plain byte store (no atomics: a stale read only delays a flag to the next pass). Every id in C is
 //      connected to h by edges of this batch, so C lies inside one component of the folded forest;
-//      gmin = min C (block minimum, one atomicMin only when it beats the current value);
+//      gmin = min C: each block stores its minimum discovery in a slot of its own, the last pack reduces them;
 //  (3) seed_init_kernel: parent[v] = (v ∈ C) ? gmin : UNSEEN and the bitmap of C — the reset and all of C's
 //      union work in one pass. The filtered kernel then folds the WHOLE batch against C: edges inside C are
 //      skipped, every other edge (prefix included) takes the union path, so the result is exact.
 // ------------------------------------------------------------------------------------------------
 constexpr int kHubBlock = 1024;
-constexpr u32 kHubSlots = 16384;  // LDS open-addressing table (key, count): 128 KiB, load factor <= 1/4
+constexpr u32 kHubSlots = 4096;  // LDS open-addressing table (key, count): 32 KiB, load factor <= 1/2
 constexpr u32 kHubProbe = 64;
-constexpr u64 kHubSample = 2048;  // edges sampled for the hub vote (2 per thread)
+constexpr u64 kHubSample = 1024;  // edges sampled for the hub vote (1 per thread)
 
 __device__ __forceinline__ void hub_count(u32 x, u32* s_key, u32* s_cnt) {
     u32 s = (u32)(gcc_splitmix64(x) & (kHubSlots - 1));
@@ -457,17 +466,24 @@ __device__ __forceinline__ bool hub_better(u32 c, u32 k, u32 bc, u32 bk) { retur
 // The hub election of one 1024-thread block: h = the most frequent endpoint of the first n_sample (<= 2048)
 // edges, ties to the smaller id — deterministic, so every block that runs it elects the same h. s_tab: 2 x
 // kHubSlots u32 of LDS (free again on return). Every thread returns h.
-__device__ __forceinline__ u32 hub_elect(const u64* __restrict__ edges, u64 n_sample, u32* s_tab) {
-    u32* s_key = s_tab;
-    u32* s_cnt = s_tab + kHubSlots;
-    __shared__ u32 s_bc[kHubBlock / 64], s_bk[kHubBlock / 64];
-    constexpr int kPer = (int)(kHubSample / kHubBlock);
-    u64 e[kPer];
+constexpr int kHubPer = (int)(kHubSample / kHubBlock);  // sample edges per thread
+
+// This thread's share of the election sample (hub_elect's input). A caller that also streams edges issues
+// these loads first: a wave's loads return in order, so a sample load queued behind the stream's first round
+// would hold the election until that whole round had arrived.
+__device__ __forceinline__ void hub_sample(const u64* __restrict__ edges, u64 n_sample, u64 (&e)[kHubPer]) {
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {  // all sample loads in flight at once
+    for (int k = 0; k < kHubPer; ++k) {  // all sample loads in flight at once
         const u64 i = threadIdx.x + (u64)k * kHubBlock;
         e[k] = i < n_sample ? edges[i] : ~0ull;
     }
+}
+
+__device__ __forceinline__ u32 hub_elect(const u64 (&e)[kHubPer], u32* s_tab) {
+    u32* s_key = s_tab;
+    u32* s_cnt = s_tab + kHubSlots;
+    __shared__ u32 s_bc[kHubBlock / 64], s_bk[kHubBlock / 64];
+    constexpr int kPer = kHubPer;
     {
         const u32x4 kz = {UNSEEN, UNSEEN, UNSEEN, UNSEEN}, cz = {0, 0, 0, 0};
         for (u32 s = threadIdx.x; s < kHubSlots / 4; s += kHubBlock) {
@@ -519,7 +535,9 @@ __global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restri
                                                              u8* __restrict__ flags, u32* __restrict__ bits32, u32 n,
                                                              u32* __restrict__ gmin) {
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
-    const u32 h = hub_elect(edges, n_sample, s_dyn);
+    u64 e[kHubPer];
+    hub_sample(edges, n_sample, e);
+    const u32 h = hub_elect(e, s_dyn);
     // this block's share: 32 ids per unit = 32 flag bytes (two 16-B stores) + one bitmap word
     const u64 nu = ((u64)n + 31) / 32;
     const u64 per = (nu + gridDim.x - 1) / gridDim.x;
@@ -538,7 +556,7 @@ __global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restri
         f4[2 * u + 1] = z1;
         bits32[u] = w;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *gmin = h;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *gmin = h;  // the hub's own slot of the seeding's minimum
 }
 
 // One BFS pass over the prefix. LDS = true: every block (one per CU) holds the bitmap of C as of the last
@@ -550,7 +568,7 @@ __global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restri
 template <bool LDS, int BLOCK, bool NT, bool HUB>
 __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__ edges, u64 n,
                                                          const u32* __restrict__ bits32, u32 nwords32,
-                                                         u8* __restrict__ flags, u32* __restrict__ gmin, u8 epoch) {
+                                                         u8* __restrict__ flags, u32* __restrict__ bmin, u8 epoch) {
     static_assert(!HUB || (LDS && BLOCK == kHubBlock), "the fused hub election needs the LDS variant");
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     __shared__ u32 s_min;
@@ -566,15 +584,21 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
     const u64 stride = (u64)gridDim.x * BLOCK;
     const u64 i = (u64)blockIdx.x * BLOCK + threadIdx.x;
     const u64 cnt = i < n2 ? (n2 - 1 - i) / stride + 1 : 0;
+    u64 e[kHubPer];
+    if constexpr (HUB) hub_sample(edges, n < kHubSample ? n : kHubSample, e);  // ahead of the stream (hub_sample)
     u32x4 q[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k)  // the first round is in flight while the bitmap is copied into LDS
-        if ((u64)k < cnt) q[k] = ld(body + i + k * stride);
+    for (int k = 0; k < D; ++k) {  // the first round is in flight while the bitmap is copied into LDS
+        // unconditional (clamped in range; launch_seed guarantees n2 >= 1): the compiler can then count them
+        // and wait for the sample alone before the election
+        const u64 j = i + k * stride;
+        q[k] = ld(body + (j < n2 ? j : n2 - 1));
+    }
     u32* bm = const_cast<u32*>(bits32);
     if (threadIdx.x == 0) s_min = UNSEEN;
     u32 lmin = UNSEEN;
     if constexpr (HUB) {
-        const u32 h = hub_elect(edges, n < kHubSample ? n : kHubSample, s_dyn);  // ends with a barrier
+        const u32 h = hub_elect(e, s_dyn);  // ends with a barrier
         const u32x4 z = {0, 0, 0, 0};
         for (u32 w = threadIdx.x; w < nwords32 / 4; w += BLOCK) reinterpret_cast<u32x4*>(s_dyn)[w] = z;
         __syncthreads();
@@ -626,27 +650,30 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
     for (int off = 32; off > 0; off >>= 1) lmin = min(lmin, (u32)__shfl_down(lmin, off, 64));
     if ((threadIdx.x & 63) == 0 && lmin != UNSEEN) atomicMin(&s_min, lmin);
     __syncthreads();
-    // one global atomic only for a new record (same-address atomics serialise at the memory side)
-    if (threadIdx.x == 0 && s_min < __hip_atomic_load(gmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMin(gmin, s_min);
+    // the block's minimum discovery, in its own slot (seed_pack_kernel<true> reduces the slots): no global atomic
+    if (threadIdx.x == 0) bmin[blockIdx.x] = s_min;
 }
 
 // Pack the flag bytes into the bitmap of C (8 lanes = one u32 word, 4 ids per lane). PARENT = true (the
 // last step of the seeding): also parent[v] = (v in C) ? gmin : UNSEEN with 16-B stores, and publish gmin as
 // the tracked component.
-// A flag byte marks C iff it equals the seeding's epoch. PARENT also re-arms gmin_next (the other gmin slot,
-// which the next seeding's atomicMins start from).
+// A flag byte marks C iff it equals the seeding's epoch.
 template <bool PARENT>
 __global__ __launch_bounds__(kBlock) void seed_pack_kernel(u32* __restrict__ parent, u32 n, const u8* __restrict__ flags,
-                                                           u32* __restrict__ bits32, const u32* __restrict__ gmin,
-                                                           u32* __restrict__ giant, u8 epoch, u32* __restrict__ gmin_next) {
+                                                           u32* __restrict__ bits32, const u32* __restrict__ bmin,
+                                                           u32 n_bmin, u32* __restrict__ giant, u8 epoch) {
     u32 g = 0;
-    if constexpr (PARENT) {
-        g = *gmin;
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            *giant = g;
-            if (gmin_next) *gmin_next = UNSEEN;
-        }
+    if constexpr (PARENT) {  // g = min C = the minimum of the BFS blocks' (and the hub's) slots
+        __shared__ u32 s_g[kBlock / 64];
+        u32 m = UNSEEN;
+        for (u32 j = threadIdx.x; j < n_bmin; j += kBlock) m = min(m, bmin[j]);
+        for (int off = 32; off > 0; off >>= 1) m = min(m, (u32)__shfl_down(m, off, 64));
+        if ((threadIdx.x & 63) == 0) s_g[threadIdx.x >> 6] = m;
+        __syncthreads();
+        g = s_g[0];
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) g = min(g, s_g[w]);
+        if (blockIdx.x == 0 && threadIdx.x == 0) *giant = g;
     }
     const u32 ep4 = 0x01010101u * epoch;
     const u64 stride = (u64)gridDim.x * kBlock;
@@ -936,15 +963,15 @@ struct gcc_forest {
 
     // giant-component filter: bitmap of one component (valid forever: components only grow)
     u64* d_bits = nullptr;
-    u32* d_giant = nullptr;  // [0], [1]: tracked-component root slots; [2]: seed gmin
+    u32* d_giant = nullptr;  // [0], [1]: tracked-component root slots
     bool has_giant = false;
     int giant_slot = 0;  // d_giant[giant_slot] = root of the tracked component as of the last refresh
     u32* d_qcount = nullptr;  // per-block slow-edge counts of the last filtered launch (measurement)
     // fused seeding: dedicated flag bytes (one per id, rounded up to a bitmap word), marked with an epoch
-    // 1..255 so they need clearing once per 255 seedings; gmin slot d_giant[2 + seeds % 2]
+    // 1..255 so they need clearing once per 255 seedings
     u8* d_flags = nullptr;
     u32 flag_epoch = 0;  // the last epoch written into d_flags (0: needs clearing)
-    u64 seeds = 0;
+    u32* d_bmin = nullptr;  // seeding: per-block minima of the BFS passes (seed_pack_kernel<true> reduces them)
 
     // pinned double-buffered staging for host-fed edges (per-edge foldEdges appends here)
     static constexpr u64 kStageEdges = 1ull << 20;  // 8 MiB per slot
@@ -1042,7 +1069,6 @@ static int alloc_filter(gcc_forest* h) {
     if (h->d_bits) return GCC_OK;
     HIP_TRY(hipMalloc((void**)&h->d_bits, (size_t)h->nwords() * sizeof(u64) + 16));
     HIP_TRY(hipMalloc((void**)&h->d_giant, 4 * sizeof(u32)));
-    HIP_TRY(hipMemsetAsync(h->d_giant, 0xFF, 4 * sizeof(u32), h->stream));  // both gmin slots start at UNSEEN
     return GCC_OK;
 }
 
@@ -1149,10 +1175,10 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u32 nw32 = 2 * (h->nwords() + (h->nwords() & 1));  // u32 bitmap words, rounded to 16 B
     const bool lds = nw32 / 2 <= kLdsBitmapMaxWords;
     const bool fuse = t.seed_fuse && lds && t.seed_passes > 0;
-    // gmin slot of this seeding (re-armed to UNSEEN by the previous seeding's last pack, or at allocation)
-    const u64 seed_no = h->seeds++;
-    u32* gmin = h->d_giant + 2 + (seed_no & 1);
-    u32* gmin_next = h->d_giant + 2 + ((seed_no + 1) & 1);
+    // per-block minimum slots: [0] the hub (seed_hub_kernel; unused when fused), then one per BFS block and pass
+    if (!h->d_bmin) HIP_TRY(hipMalloc((void**)&h->d_bmin, (1 + 16 * (size_t)kMaxGrid) * sizeof(u32)));
+    u32* gmin = h->d_bmin;
+    u32 n_bmin = 1;
     u8* flags;
     u8 epoch = 1;
     if (fuse) {  // dedicated epoch-marked flags: nothing to clear
@@ -1180,9 +1206,10 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
                       edges, std::min(n, kHubSample), flags, bits, h->cap, gmin);
         if (rc) return rc;
     }
-    const u64 pref = std::min(n, std::max<u64>(t.filter_min_batch, n / std::max<u64>(1, t.seed_div)));
+    // BFS prefixes hold at least 64 edges (the kernel's clamped loads need a non-empty body; n >= 64 here)
+    const u64 pref = std::min(n, std::max<u64>({64, t.filter_min_batch, n / std::max<u64>(1, t.seed_div)}));
     // the first pass only has to reach the hubs next to h: a shorter prefix
-    const u64 pref1 = std::min(pref, std::max<u64>(t.filter_min_batch, n / std::max<u64>(1, t.seed_div1)));
+    const u64 pref1 = std::min(pref, std::max<u64>({64, t.filter_min_batch, n / std::max<u64>(1, t.seed_div1)}));
     const unsigned pack_grid = grid_for(((u64)h->cap + 3) / 4, kMaxGrid);
     for (int p = 0; p < t.seed_passes; ++p) {
         const u64 np = p == 0 ? pref1 : pref;
@@ -1202,26 +1229,30 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
             const size_t sh = std::max<size_t>((size_t)nw32 * sizeof(u32), hub ? 2 * kHubSlots * sizeof(u32) : 0);
 #define GCC_BFS(NT, HUB)                                                                                       \
     launch_k(h, "seed_bfs", np, seed_bfs_kernel<true, kFilterBlockLds, NT, HUB>, dim3(h->n_cu), dim3(kFilterBlockLds), \
-             sh, edges, np, (const u32*)bits, nw32, flags, gmin, epoch)
+             sh, edges, np, (const u32*)bits, nw32, flags, h->d_bmin + n_bmin, epoch)
             rc = t.seed_nt ? (hub ? GCC_BFS(true, true) : GCC_BFS(true, false))
                            : (hub ? GCC_BFS(false, true) : GCC_BFS(false, false));
 #undef GCC_BFS
         } else {
             const unsigned grid = grid_for((np + 1) / 2, kMaxGrid);
             rc = t.seed_nt ? launch_k(h, "seed_bfs", np, seed_bfs_kernel<false, kBlock, true, false>, dim3(grid),
-                                      dim3(kBlock), 0, edges, np, (const u32*)bits, nw32, flags, gmin, epoch)
+                                      dim3(kBlock), 0, edges, np, (const u32*)bits, nw32, flags, h->d_bmin + n_bmin, epoch)
                            : launch_k(h, "seed_bfs", np, seed_bfs_kernel<false, kBlock, false, false>, dim3(grid),
-                                      dim3(kBlock), 0, edges, np, (const u32*)bits, nw32, flags, gmin, epoch);
+                                      dim3(kBlock), 0, edges, np, (const u32*)bits, nw32, flags, h->d_bmin + n_bmin, epoch);
+            n_bmin += grid;
         }
         if (rc) return rc;
+        if (lds) n_bmin += (u32)h->n_cu;
         if (p + 1 < t.seed_passes) {
             rc = launch_k(h, "seed_pack", 0, seed_pack_kernel<false>, dim3(pack_grid), dim3(kBlock), 0, h->d_parent, h->cap,
-                          (const u8*)flags, bits, (const u32*)gmin, h->d_giant + h->giant_slot, epoch, (u32*)nullptr);
+                          (const u8*)flags, bits, (const u32*)nullptr, 0u, h->d_giant + h->giant_slot, epoch);
             if (rc) return rc;
         }
     }
+    // fused: slot 0 (the hub's) is not written; h is in block 0's slot of the first pass
     rc = launch_k(h, "seed_init", 0, seed_pack_kernel<true>, dim3(pack_grid), dim3(kBlock), 0, h->d_parent, h->cap,
-                  (const u8*)flags, bits, (const u32*)gmin, h->d_giant + h->giant_slot, epoch, gmin_next);
+                  (const u8*)flags, bits, (const u32*)(fuse ? h->d_bmin + 1 : h->d_bmin), fuse ? n_bmin - 1 : n_bmin,
+                  h->d_giant + h->giant_slot, epoch);
     if (rc) return rc;
     h->pending_reset = false;
     h->has_giant = true;
@@ -1247,6 +1278,7 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
     // measured faster (profiles/r1_sweep_c4_seed.log)
     const bool seed_fits = (u64)h->nwords() + (h->nwords() & 1) <= kLdsBitmapMaxWords || t.seed_global;
     const bool seeded = h->pending_reset && h->filter_enabled() && t.seed && seed_fits && n >= t.filter_min_batch &&
+                        n >= 64 &&
                         ((reinterpret_cast<uintptr_t>(h->d_parent) | reinterpret_cast<uintptr_t>(h->d_spare)) & 15) == 0;
     double refresh[3] = {t.refresh[0], t.refresh[1], t.refresh[2]};
     if (seeded) {
@@ -1486,6 +1518,7 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (h->d_bits) (void)hipFree(h->d_bits);
     if (h->d_giant) (void)hipFree(h->d_giant);
     if (h->d_flags) (void)hipFree(h->d_flags);
+    if (h->d_bmin) (void)hipFree(h->d_bmin);
     if (h->d_qcount) (void)hipFree(h->d_qcount);
     if (h->d_counts) (void)hipFree(h->d_counts);
     for (auto& pe : h->kev) {

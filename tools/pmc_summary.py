@@ -26,14 +26,19 @@ def main():
     w = per_kernel(f"{d}/write/run_counter_collection.csv", "WRITE_SIZE")
     h = per_kernel(f"{d}/hit/run_counter_collection.csv", "TCC_HIT_sum")
     m = per_kernel(f"{d}/hit/run_counter_collection.csv", "TCC_MISS_sum")
-    name = next(k for k in f if ksub in k)
-    fetch_kb = sum(f[name]) / len(f[name])
-    write_kb = sum(w[name]) / len(w[name])
-    hit, miss = sum(h[name]) / len(h[name]), sum(m[name]) / len(m[name])
+    names = [k for k in f if ksub in k]  # every instantiation of the kernel (same units per launch)
+    fv = [x for k in names for x in f[k]]
+    wv = [x for k in names for x in w.get(k, [])]
+    hv = [x for k in names for x in h.get(k, [])]
+    mv = [x for k in names for x in m.get(k, [])]
+    fetch_kb = sum(fv) / len(fv)
+    write_kb = sum(wv) / len(wv)
+    hit, miss = sum(hv) / len(hv), sum(mv) / len(mv)
     rec = {
         "workload": workload,
-        "kernel": name,
-        "launches_sampled": len(f[name]),
+        "kernel": names[0] if len(names) == 1 else ksub,
+        "instantiations": names,
+        "launches_sampled": len(fv),
         "edges_per_launch": edges,
         "fetch_size_kb": fetch_kb,
         "write_size_kb": write_kb,
