@@ -104,17 +104,29 @@ constexpr u32 kRing = 128;  // u64 entries per wave (1 KiB): pending stays < 64 
 
 // One drain round: the wave unites up to 64 ring entries, one per lane. Out of line: it runs rarely, and
 // inlined at each of the hot loop's 8 push sites it multiplied the loop body ~8x (I-cache, registers).
-__device__ __attribute__((noinline)) void ring_drain(const u64* ring, u32 wd, u32 pending, u32* parent) {
+// The union of one ring entry. An entry (g, x) with x > g (an edge from the tracked component to an id outside
+// it) takes the hook of filter_round: ONE atomicMin(parent[x], g); only if x already hung under some other id
+// p (old not in {UNSEEN, x, g}) is the link to p restored by union(g, p). Anything else: the full union.
+__device__ __forceinline__ void unite_entry(u32* parent, u32 a, u32 b, u32 g) {
+    NoCount c;
+    if (a == g && b > g) {
+        const u32 old = atomicMin(&parent[b], g);
+        if (old != UNSEEN && old != b && old != g) UF::unite(parent, g, old, c);
+    } else {
+        UF::unite(parent, a, b, c);
+    }
+}
+
+__device__ __attribute__((noinline)) void ring_drain(const u64* ring, u32 wd, u32 pending, u32* parent, u32 g) {
     const u32 lane = threadIdx.x & 63;
     if (lane < pending) {
         const u64 e = ring[(wd + lane) & (kRing - 1)];
-        NoCount c;
-        UF::unite(parent, (u32)e, (u32)(e >> 32), c);
+        unite_entry(parent, (u32)e, (u32)(e >> 32), g);
     }
 }
 
 __device__ __forceinline__ void ring_push(bool slow, u32 a, u32 b, u64* ring, u32& wq, u32& wd, u32* parent,
-                                          u32 drain_at) {
+                                          u32 drain_at, u32 g) {
     const unsigned long long m = __ballot(slow);
     if (m == 0) return;
     const u32 lane = threadIdx.x & 63;
@@ -122,7 +134,7 @@ __device__ __forceinline__ void ring_push(bool slow, u32 a, u32 b, u64* ring, u3
     wq += (u32)__popcll(m);
     const u32 pending = wq - wd;
     if (pending >= drain_at) {  // wave-uniform: drain one round (up to 64 edges), one edge per lane
-        ring_drain(ring, wd, pending, parent);
+        ring_drain(ring, wd, pending, parent, g);
         wd += pending < 64 ? pending : 64;
     }
 }
@@ -134,7 +146,8 @@ template <bool LDS>
 __device__ __forceinline__ void filter_edge(bool valid, u32 a, u32 b, const u32* bm, u32 g, u64* ring, u32& wq,
                                             u32& wd, u32* parent, u32 drain_at) {
     const u32 ia = in_c<LDS>(bm, a), ib = in_c<LDS>(bm, b);
-    ring_push(valid && !(ia & ib), ia ? g : a, ib ? g : b, ring, wq, wd, parent, drain_at);
+    // (g, other end) when exactly one end is in C: the drain's hook form (unite_entry)
+    ring_push(valid && !(ia & ib), ia ? g : (ib ? g : a), ia ? b : (ib ? a : b), ring, wq, wd, parent, drain_at, g);
 }
 
 // A round of N edges of the filtered stream with the direct hook (HOOK): an edge with exactly one end in C and
@@ -157,7 +170,7 @@ struct HookCarry {
 #pragma unroll
         for (int k = 0; k < N; ++k) {
             const bool again = hook[k] && old[k] != GCC_UNSEEN && old[k] != other[k] && old[k] != g;
-            ring_push(again, g, again ? old[k] : 0u, ring, wq, wd, parent, drain_at);
+            ring_push(again, g, again ? old[k] : 0u, ring, wq, wd, parent, drain_at, g);
         }
     }
 };
@@ -186,7 +199,7 @@ __device__ __forceinline__ void filter_round(const bool* valid, const u32* a, co
     }
     carry.settle(g, ring, wq, wd, parent, drain_at);  // the previous round's hooks (their atomics have returned)
 #pragma unroll
-    for (int k = 0; k < N; ++k) ring_push(slow[k], pa[k], pb[k], ring, wq, wd, parent, drain_at);
+    for (int k = 0; k < N; ++k) ring_push(slow[k], pa[k], pb[k], ring, wq, wd, parent, drain_at, g);
     carry = cur;
 }
 
@@ -308,7 +321,7 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
     for (; wd < wq; wd += 64) {
         if (lane < wq - wd) {
             const u64 e = ring[(wd + lane) & (kRing - 1)];
-            UF::unite(parent, (u32)e, (u32)(e >> 32), c);
+            unite_entry(parent, (u32)e, (u32)(e >> 32), g);
         }
     }
     if (lane == 0 && wq) atomicAdd(&s_slow, wq);

@@ -254,6 +254,25 @@ def test_order_invariance_and_idempotence(torch_cuda):
         x.close()
 
 
+def test_seeded_fold_across_flag_epochs(torch_cuda):
+    """The seeding marks C with flag bytes holding an epoch 1..255 (cleared once per 255 seedings) and keeps
+    per-block minima: 300 reset + fold cycles of one R-MAT batch (crossing the wrap) must all give the oracle's
+    labels, with the fused and the separate hub election and several BFS prefixes."""
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=17, n_edges=1 << 20)
+    E, V = cfg.info()
+    want = orc.cc_stream(G.generate_host(cfg), [0, E], V, partitions=2, threads=2)
+    d = device_stream(torch_cuda, cfg)
+    ds = DisjointSet(V)
+    knobs = [{}, {"seed_fuse": 0}, {"seed_div": 2, "seed_div1": 4}, {"seed_passes": 1}, {"seed_passes": 3}]
+    for i in range(300):
+        ds.tune(**{"seed_fuse": 1, "seed_div": 3, "seed_div1": 3, "seed_passes": 2, **knobs[i % len(knobs)]})
+        ds.reset()
+        ds.fold_device(d.data_ptr(), E)
+        if i % 7 == 0 or i >= 250:
+            assert orc.label_digest(ds.labels()) == int(want["digest"][0]), i
+    ds.close()
+
+
 def test_edge_cases():
     ds = DisjointSet(1 << 10)
     ds.fold(np.zeros((0, 2), dtype=np.uint32))  # empty batch
