@@ -780,20 +780,27 @@ __global__ __launch_bounds__(kBlock) void msg_encode_kernel(const u32* __restric
     }
 }
 
-__global__ void msg_header_kernel(u32* __restrict__ hdr, const u32* __restrict__ giant_root, u32 has_giant, u32 n) {
-    hdr[0] = has_giant ? *giant_root : UNSEEN;
-    hdr[1] = 0;
-    hdr[2] = n;
-    hdr[3] = 0;
+// One wave: the header, and the witness slots of the absorb that follows a merge's all_gather re-armed to UNSEEN
+// (saves that absorb a memset launch).
+__global__ void msg_header_kernel(u32* __restrict__ hdr, const u32* __restrict__ giant_root, u32 has_giant, u32 n,
+                                  u32* __restrict__ witness) {
+    if (threadIdx.x == 0) {
+        hdr[0] = has_giant ? *giant_root : UNSEEN;
+        hdr[1] = 0;
+        hdr[2] = n;
+        hdr[3] = 0;
+    }
+    if (witness) witness[threadIdx.x] = UNSEEN;
 }
 
-// Absorbing the P-1 peer messages of an all_gather (gcc_forest_absorb_many), two launches:
+// Absorbing the P-1 peer messages of an all_gather (gcc_forest_absorb_many), three launches:
 //  msg_overlap_kernel: for each peer p, does its giant G_p share an id with this forest's tracked component T
 //    (bitmap `mine`, root R; valid forever since components only grow)? If so, witness[p] = one shared id.
-//  msg_absorb_kernel: for the overlapping peers, unite(witness_p, g_p) joins G_p's root to T (block 0), after
-//    which every id of G_p is connected to R — so the union U of their bitmaps only needs its ids OUTSIDE T
-//    united with R, each ONCE however many peers hold it (one 64-id word per wave, one id per lane). Peers
-//    without overlap (or no T at all) are absorbed id by id against their own root. Then the (v, label) lists.
+//  msg_absorb_bits_kernel: an overlapping peer's giant G_p is connected to T (root R) through the witness, so
+//    the union U of their bitmaps only needs its ids OUTSIDE T joined to R, each ONCE however many peers hold it
+//    (one 64-id word per wave, one id per lane); a new id above R by a plain store;
+//  msg_absorb_kernel: the giants without overlap (or all of them when there is no T: id by id against their
+//    own root), then the (v, label) lists.
 constexpr u32 kMaxPeers = 64;
 
 __global__ __launch_bounds__(kBlock) void msg_overlap_kernel(const char* __restrict__ msgs, u64 stride, u32 count,
@@ -818,68 +825,102 @@ __global__ __launch_bounds__(kBlock) void msg_overlap_kernel(const char* __restr
     }
 }
 
-__global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ parent, const char* __restrict__ msgs,
-                                                            u64 stride, u32 count, u32 skip, u64 cap, u32 n,
-                                                            const u64* __restrict__ mine, const u32* __restrict__ tracked,
-                                                            const u32* __restrict__ witness) {
-    __shared__ u32 s_g[kMaxPeers];
-    __shared__ u32 s_w[kMaxPeers];
-    NoCount c;
-    const u32 lane = threadIdx.x & 63;
+// Peer p's giant root g_p and its witness (an id shared with T), or UNSEEN; the same in every block.
+__device__ __forceinline__ void msg_peers(const char* __restrict__ msgs, u64 stride, u32 count, u32 skip, u32 n,
+                                          bool tracked, const u32* __restrict__ witness, u32* s_g, u32* s_w) {
     if (threadIdx.x < kMaxPeers) {
         u32 g = UNSEEN, wv = UNSEEN;
         if (threadIdx.x < count && threadIdx.x != skip) {
             const u32* hdr = reinterpret_cast<const u32*>(msgs + threadIdx.x * stride);
             if (hdr[2] == n && hdr[0] < n) {
                 g = hdr[0];
-                wv = mine ? witness[threadIdx.x] : UNSEEN;
+                wv = tracked ? witness[threadIdx.x] : UNSEEN;
             }
         }
         s_g[threadIdx.x] = g;
         s_w[threadIdx.x] = wv;
-        if (blockIdx.x == 0 && wv != UNSEEN && wv != g) UF::unite(parent, wv, g, c);  // G_p joins T
     }
     __syncthreads();
-    const u32 R = mine ? *tracked : UNSEEN;
+}
+
+// Absorb, phase 1 (after msg_overlap_kernel): the union U of the giants that meet T, minus T, one 64-id word per
+// wave, each id once however many peers hold it. Every id of such a giant is connected to T (through the
+// witness), so x in U \ T joins T's root R. A new id above R — the common case — is hung under R by a PLAIN
+// store: in this kernel x has no other writer (each id belongs to one lane, and the other lanes' unions only
+// CAS roots of trees of seen ids), and the witness and list unions, which could also touch it, run in phase 2.
+// Anything else takes the full union.
+__global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict__ parent, const char* __restrict__ msgs,
+                                                                 u64 stride, u32 count, u32 skip, u32 n,
+                                                                 const u64* __restrict__ mine,
+                                                                 const u32* __restrict__ tracked,
+                                                                 const u32* __restrict__ witness) {
+    __shared__ u32 s_g[kMaxPeers];
+    __shared__ u32 s_w[kMaxPeers];
+    msg_peers(msgs, stride, count, skip, n, true, witness, s_g, s_w);
+    NoCount c;
+    const u32 lane = threadIdx.x & 63;
+    const u32 R = *tracked;
     const u64 nw = ((u64)n + 63) / 64;
     const u64 wave = (u64)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const u64 waves = (u64)gridDim.x * (kBlock / 64);
     for (u64 w = wave; w < nw; w += waves) {
         // lane p < count loads peer p's word; the overlapping peers' words are OR-ed across the wave
-        u64 m = 0, lone = 0;
-        if (lane < count && s_g[lane] != UNSEEN) {
+        u64 m = 0;
+        if (lane < count && s_g[lane] != UNSEEN && s_w[lane] != UNSEEN)
             m = reinterpret_cast<const u64*>(msgs + lane * stride + GCC_MSG_HEADER_BYTES)[w];
-            if (s_w[lane] == UNSEEN) {
-                lone = m;  // no overlap with T: absorbed against its own root below
-                m = 0;
-            }
-        }
         for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off, 64);
-        const u64 v = w * 64 + lane;
-        if (m) {
-            const u64 todo = m & ~mine[w];
-            if (((todo >> lane) & 1ull) && (u32)v != R) UF::unite(parent, (u32)v, R, c);
-        }
-        unsigned long long lb = __ballot(lone != 0);
-        while (lb) {  // rare: peers whose giant does not touch T (or no T)
-            const u32 p = (u32)__builtin_ctzll(lb);
-            lb &= lb - 1;
-            const u64 mp = __shfl(lone, (int)p, 64);
-            if (((mp >> lane) & 1ull) && (u32)v != s_g[p]) UF::unite(parent, (u32)v, s_g[p], c);
+        if (!m) continue;
+        const u64 todo = m & ~mine[w];
+        const u32 v = (u32)(w * 64 + lane);
+        if (((todo >> lane) & 1ull) && v != R) {
+            if (v > R && parent[v] == UNSEEN) parent[v] = R;  // new id: seen and hung under R in one store
+            else UF::unite(parent, v, R, c);
         }
     }
+}
+
+// Absorb, phase 2 (or the whole absorb when this forest tracks no component): the giants that do not meet T
+// (each id against its own root g_p) and every peer's (v, label) list.
+__global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ parent, const char* __restrict__ msgs,
+                                                            u64 stride, u32 count, u32 skip, u64 cap, u32 n,
+                                                            bool tracked, const u32* __restrict__ witness) {
+    __shared__ u32 s_g[kMaxPeers];
+    __shared__ u32 s_w[kMaxPeers];
+    msg_peers(msgs, stride, count, skip, n, tracked, witness, s_g, s_w);
+    NoCount c;
+    // (an overlapping peer's giant needs no union of its own: phase 1 joined every id of it outside T to R)
+    const u32 lane = threadIdx.x & 63;
+    const u64 nw = ((u64)n + 63) / 64;
+    const u64 wave = (u64)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const u64 waves = (u64)gridDim.x * (kBlock / 64);
+    bool any_lone = false;
+    for (u32 p = 0; p < count; ++p) any_lone |= s_g[p] != UNSEEN && s_w[p] == UNSEEN;
+    if (any_lone) {  // rare: peers whose giant does not touch T (or no T)
+        for (u64 w = wave; w < nw; w += waves) {
+            u64 lone = 0;
+            if (lane < count && s_g[lane] != UNSEEN && s_w[lane] == UNSEEN)
+                lone = reinterpret_cast<const u64*>(msgs + lane * stride + GCC_MSG_HEADER_BYTES)[w];
+            const u64 v = w * 64 + lane;
+            unsigned long long lb = __ballot(lone != 0);
+            while (lb) {
+                const u32 p = (u32)__builtin_ctzll(lb);
+                lb &= lb - 1;
+                const u64 mp = __shfl(lone, (int)p, 64);
+                if (((mp >> lane) & 1ull) && (u32)v != s_g[p]) UF::unite(parent, (u32)v, s_g[p], c);
+            }
+        }
+    }
+    // the lists as one flat index over (peer, entry): one header load per entry, every union in flight at once
     const u64 stride_t = (u64)gridDim.x * kBlock;
-    const u64 tid = (u64)blockIdx.x * kBlock + threadIdx.x;
-    for (u32 p = 0; p < count; ++p) {
+    for (u64 t = (u64)blockIdx.x * kBlock + threadIdx.x; t < (u64)count * cap; t += stride_t) {
+        const u32 p = (u32)(t / cap);
+        const u64 k = t - (u64)p * cap;
         if (p == skip) continue;
         const u32* hdr = reinterpret_cast<const u32*>(msgs + p * stride);
-        if (hdr[2] != n) continue;
+        if (hdr[2] != n || k >= min((u64)hdr[1], cap)) continue;
         const u32* others = reinterpret_cast<const u32*>(msgs + p * stride + GCC_MSG_HEADER_BYTES + nw * sizeof(u64));
-        const u64 cnt = min((u64)hdr[1], cap);
-        for (u64 k = tid; k < cnt; k += stride_t) {
-            const u32 v = others[2 * k], l = others[2 * k + 1];
-            if (v < n && l < n) UF::unite(parent, v, l, c);
-        }
+        const u32 v = others[2 * k], l = others[2 * k + 1];
+        if (v < n && l < n) UF::unite(parent, v, l, c);
     }
 }
 
@@ -997,6 +1038,7 @@ struct gcc_forest {
     // scratch for cross-device merges
     u32* d_scratch = nullptr;
     u32* d_witness = nullptr;  // absorb_many: per-peer id shared with the tracked component
+    bool witness_armed = false;  // the last encode already reset d_witness (stream-ordered before the next absorb)
 
     unsigned long long* d_counts = nullptr;
 
@@ -1754,8 +1796,10 @@ int gcc_forest_encode(gcc_forest* h, void* d_msg, uint64_t cap_others) {
     u32* hdr = reinterpret_cast<u32*>(d_msg);
     u64* bits = reinterpret_cast<u64*>(static_cast<char*>(d_msg) + GCC_MSG_HEADER_BYTES);
     u32* others = reinterpret_cast<u32*>(bits + ((u64)h->cap + 63) / 64);
-    hipLaunchKernelGGL(msg_header_kernel, dim3(1), dim3(1), 0, h->stream, hdr,
-                       h->d_giant ? h->d_giant + h->giant_slot : hdr, h->has_giant ? 1u : 0u, h->cap);
+    if (!h->d_witness) HIP_TRY(hipMalloc((void**)&h->d_witness, kMaxPeers * sizeof(u32)));
+    hipLaunchKernelGGL(msg_header_kernel, dim3(1), dim3(kMaxPeers), 0, h->stream, hdr,
+                       h->d_giant ? h->d_giant + h->giant_slot : hdr, h->has_giant ? 1u : 0u, h->cap, h->d_witness);
+    h->witness_armed = true;
     const u64 nw = ((u64)h->cap + 63) / 64;
     hipLaunchKernelGGL(msg_encode_kernel, dim3((unsigned)((nw + kMsgWordsPerBlock - 1) / kMsgWordsPerBlock)), dim3(kBlock),
                        0, h->stream, h->d_parent, h->cap, hdr, bits, others, (u64)cap_others);
@@ -1779,14 +1823,21 @@ int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_by
     const char* msgs = static_cast<const char*>(d_msgs);
     if (tracked) {
         if (!h->d_witness) HIP_TRY(hipMalloc((void**)&h->d_witness, kMaxPeers * sizeof(u32)));
-        HIP_TRY(hipMemsetAsync(h->d_witness, 0xFF, kMaxPeers * sizeof(u32), h->stream));
+        if (!h->witness_armed) HIP_TRY(hipMemsetAsync(h->d_witness, 0xFF, kMaxPeers * sizeof(u32), h->stream));
+        h->witness_armed = false;
         hipLaunchKernelGGL(msg_overlap_kernel, dim3(grid_for((u64)count * ((nw + 63) / 64) * 64, kMaxGrid)), dim3(kBlock),
                            0, h->stream, msgs, (u64)stride_bytes, count, skip, h->cap, mine, h->d_witness);
     }
-    const u64 work = std::max<u64>(nw * 64, cap_others);  // one word per wave; one list entry per lane
+    // one list entry per lane; with no tracked component every giant goes id by id too (one word per wave)
+    const u64 lists = std::max<u64>((u64)count * cap_others, 1);
+    const u64 work = tracked ? std::max<u64>(lists, 64 * kBlock) : std::max<u64>(nw * 64, lists);
+    if (tracked)
+        hipLaunchKernelGGL(msg_absorb_bits_kernel, dim3(grid_for(nw * 64, kMaxGrid)), dim3(kBlock), 0, h->stream,
+                           h->d_parent, msgs, (u64)stride_bytes, count, skip, h->cap, mine,
+                           (const u32*)(h->d_giant + h->giant_slot), (const u32*)h->d_witness);
     hipLaunchKernelGGL(msg_absorb_kernel, dim3(grid_for(work, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent, msgs,
-                       (u64)stride_bytes, count, skip, (u64)cap_others, h->cap, mine,
-                       tracked ? h->d_giant + h->giant_slot : nullptr, tracked ? h->d_witness : nullptr);
+                       (u64)stride_bytes, count, skip, (u64)cap_others, h->cap, tracked,
+                       tracked ? (const u32*)h->d_witness : nullptr);
     HIP_TRY(hipGetLastError());
     mark_mutated(h);
     return GCC_OK;

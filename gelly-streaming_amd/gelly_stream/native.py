@@ -11,7 +11,8 @@ import os
 from ctypes import POINTER, byref, c_char_p, c_float, c_int, c_uint32, c_uint64, c_void_p
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libgelly_cc.so")
+# GELLY_CC_LIB: an alternative build of the same ABI (A/B measurements of kernel variants only)
+LIB_PATH = os.environ.get("GELLY_CC_LIB") or os.path.join(PKG_ROOT, "lib", "libgelly_cc.so")
 
 UNSEEN = 0xFFFFFFFF
 

@@ -355,6 +355,7 @@ def test_fold_timing_events():
 # ---- cross-GPU merge message (include/gelly_cc.h): encode / absorb, the RCCL payload's two ends ----
 def encode(torch_cuda, ds, cap):
     msg = torch_cuda.zeros(native.msg_bytes(ds.id_capacity, cap) + 16, dtype=torch_cuda.uint8, device="cuda:0")
+    torch_cuda.cuda.synchronize()  # the zero fill runs on torch's stream, the encode on the forest's own
     ds.encode_message(msg.data_ptr(), cap)
     torch_cuda.cuda.synchronize()
     hdr = msg[:16].cpu().numpy().view("<u4")

@@ -66,9 +66,9 @@ def main():
         lab.copy_(torch.from_numpy(ranks[1].labels().view("int32")).cuda())
         t = [ev() for _ in range(3)]
         t[0].record()
-        ranks[2].merge_labels_device(lab.data_ptr(), V)
+        ranks[0].merge_labels_device(lab.data_ptr(), V)
         t[1].record()
-        ranks[2].compress()
+        ranks[0].compress()
         t[2].record()
         torch.cuda.synchronize()
         print(f"butterfly round (device side): absorb labels {t[0].elapsed_time(t[1]) * 1e3:.1f} us, "
