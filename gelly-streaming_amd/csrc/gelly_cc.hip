@@ -379,8 +379,11 @@ __device__ __forceinline__ void bm_merge(u32& c1, u32& n1, u32 c2, u32 n2) {
     }
 }
 
-__global__ __launch_bounds__(1024) void giant_vote_kernel(u32* __restrict__ parent, u32 n, u32* __restrict__ giant) {
-    __shared__ u32 sc[16], sn[16];
+// share[0] = how many seen samples the winner holds, share[1] = how many samples were seen (exact counts: the
+// host turns the filter off for a forest whose largest component is no giant).
+__global__ __launch_bounds__(1024) void giant_vote_kernel(u32* __restrict__ parent, u32 n, u32* __restrict__ giant,
+                                                          u32* __restrict__ share) {
+    __shared__ u32 sc[16], sn[16], s_win, s_hit[16], s_seen[16];
     u32 l[4];
     NoCount c;
 #pragma unroll
@@ -408,7 +411,32 @@ __global__ __launch_bounds__(1024) void giant_vote_kernel(u32* __restrict__ pare
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < 16; ++w) bm_merge(sc[0], sn[0], sc[w], sn[w]);
-        *giant = sn[0] ? sc[0] : UNSEEN;
+        s_win = sn[0] ? sc[0] : UNSEEN;
+        *giant = s_win;
+    }
+    __syncthreads();
+    u32 hit = 0, seen = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        seen += l[k] != UNSEEN;
+        hit += l[k] != UNSEEN && l[k] == s_win;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        hit += __shfl_down(hit, off, 64);
+        seen += __shfl_down(seen, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        s_hit[threadIdx.x >> 6] = hit;
+        s_seen[threadIdx.x >> 6] = seen;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) {
+            s_hit[0] += s_hit[w];
+            s_seen[0] += s_seen[w];
+        }
+        share[0] = s_hit[0];
+        share[1] = s_seen[0];
     }
 }
 
@@ -984,6 +1012,7 @@ struct FoldTune {
     u64 refresh_min_batch = 1ull << 22; // batches above this refresh the giant bitmap at the refresh points
     double refresh[3] = {1.0 / 4, 0, 0};  // refresh points (fractions of the batch), increasing, 0 = unused
     bool filter = true;
+    double filter_min_share = 0.5;  // the voted component must hold this share of the seen samples (0: no check)
     int depth = 4;  // 16-B edge-pair loads in flight per lane in the filtered kernel (4 or 8)
     // seeded fold of a fresh forest (seed_* kernels): BFS from a hub over the first 1/seed_div of the batch
     bool seed = true;
@@ -1017,7 +1046,8 @@ struct gcc_forest {
 
     // giant-component filter: bitmap of one component (valid forever: components only grow)
     u64* d_bits = nullptr;
-    u32* d_giant = nullptr;  // [0], [1]: tracked-component root slots
+    u32* d_giant = nullptr;  // [0], [1]: tracked-component root slots; [4], [5]: the vote's share (giant_vote_kernel)
+    bool filter_off = false;  // the vote found no giant: this forest folds without the filter until reset
     bool has_giant = false;
     int giant_slot = 0;  // d_giant[giant_slot] = root of the tracked component as of the last refresh
     u32* d_qcount = nullptr;  // per-block slow-edge counts of the last filtered launch (measurement)
@@ -1123,7 +1153,7 @@ static int materialize_reset(gcc_forest* h) {
 static int alloc_filter(gcc_forest* h) {
     if (h->d_bits) return GCC_OK;
     HIP_TRY(hipMalloc((void**)&h->d_bits, (size_t)h->nwords() * sizeof(u64) + 16));
-    HIP_TRY(hipMalloc((void**)&h->d_giant, 4 * sizeof(u32)));
+    HIP_TRY(hipMalloc((void**)&h->d_giant, 6 * sizeof(u32)));
     return GCC_OK;
 }
 
@@ -1138,7 +1168,7 @@ static int compress_now(gcc_forest* h, const char* name = "compress") {
         if (rc) return rc;
         if (!h->has_giant)  // first refresh of this forest: elect the component to track
             rc = launch_k(h, "vote", 0, giant_vote_kernel, dim3(1), dim3(1024), 0, h->d_parent, h->cap,
-                          h->d_giant + h->giant_slot);
+                          h->d_giant + h->giant_slot, h->d_giant + 4);
         if (!rc)
             rc = launch_k(h, name, 0, compress_bits_kernel, dim3(grid_for(h->nwords() * 64ull, kMaxGrid)), dim3(kBlock), 0,
                           h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
@@ -1355,6 +1385,21 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
             b = e;
         }
         if (!rc && b < n) rc = compress_now(h, "refresh");
+        if (!rc && b < n && t.filter_min_share > 0) {
+            // once per forest: is the voted component a giant among the seen samples? If not, the filter would
+            // send almost every edge down its slow path, and the plain fold is faster (C3, C5)
+            u32 share[2] = {0, 0};
+            HIP_TRY(hipMemcpyAsync(share, h->d_giant + 4, sizeof(share), hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(hipStreamSynchronize(h->stream));
+            h->filter_off = share[0] < t.filter_min_share * share[1];
+        }
+        if (!rc && b < n && h->filter_off) {
+            rc = launch_plain(h, d_pairs + 2 * b, n - b, "plain");
+            b = n;
+        }
+    } else if (h->filter_off) {
+        rc = launch_plain(h, d_pairs, n, "plain");
+        b = n;
     }
     int next_refresh = 0;
     while (!rc && b < n) {
@@ -1633,6 +1678,7 @@ int gcc_forest_reset(gcc_forest* h) {
     h->host_valid = false;
     h->compressed = true;  // all UNSEEN is canonical
     h->has_giant = false;  // the giant bitmap described the old forest
+    h->filter_off = false;
     return GCC_OK;
 }
 
@@ -1943,6 +1989,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "seed_div1") t.seed_div1 = std::max<u64>(1, (u64)value);
     else if (k == "seed_refresh") t.seed_refresh = value;
     else if (k == "seed_fuse") t.seed_fuse = value != 0;
+    else if (k == "filter_min_share") t.filter_min_share = value;
     else return set_err(GCC_E_INVALID, "unknown tuning key '%s'", key);
     return GCC_OK;
 }
