@@ -30,6 +30,7 @@ KERNEL_BYTES = {
     "seed_bfs_kernel": (8, "edge"),         # the prefix edge stream (bitmap in LDS)
     "fold_kernel": (16, "edge"),            # edge + both parents
     "compress_bits_kernel": (8.125, "id"),  # parent read + label write + 1 bitmap bit
+    "compress_inc_kernel": (8.125, "id"),   # the same, incremental (bloom of the window's mutations in LDS)
     "seed_pack_kernel": (5.125, "id"),      # flag byte read + parent write + 1 bitmap bit (the init variant)
     "seed_hub_kernel": (1.125, "id"),       # flag byte + bitmap bit cleared
 }
@@ -203,6 +204,7 @@ def main():
     kernel_of = {"filtered": "fold_filtered_kernel", "sample": "fold_kernel", "plain": "fold_kernel",
                  "seed_hub": "seed_hub_kernel", "seed_bfs": "seed_bfs_kernel", "seed_pack": "seed_pack_kernel",
                  "seed_init": "seed_pack_kernel", "refresh": "compress_bits_kernel", "compress": "compress_bits_kernel",
+                 "compress_inc": "compress_inc_kernel", "refresh_inc": "compress_inc_kernel",
                  "vote": "giant_vote_kernel"}
     phases, kernels, spans = {}, {}, []
     for name, ms, n in log:

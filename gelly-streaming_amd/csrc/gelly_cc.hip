@@ -75,13 +75,17 @@ constexpr unsigned kMaxGrid = 2048;         // 256 CUs x 8 resident 256-thread b
 
 // Fold a batch of edges (interleaved u32 pairs) into the forest: one edge per lane per iteration, 8 B/lane
 // coalesced non-temporal stream (read once; it must not evict parent[] lines from L2).
+// REC: every id that leaves UNSEEN or root state is marked in bloom (uf_device.h BloomRec), so the next
+// compress can be incremental (compress_inc_kernel).
+template <bool REC>
 __global__ __launch_bounds__(kBlock) void fold_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
-                                                      u64 n_edges) {
+                                                      u64 n_edges, u32* __restrict__ bloom) {
     NoCount c;
     const u64 stride = (u64)gridDim.x * kBlock;
     for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n_edges; i += stride) {
         const u64 e = __builtin_nontemporal_load(edges + i);
-        UF::unite(parent, (u32)e, (u32)(e >> 32), c);
+        if constexpr (REC) UF::unite(parent, (u32)e, (u32)(e >> 32), c, gcc::BloomRec{bloom});
+        else UF::unite(parent, (u32)e, (u32)(e >> 32), c);
     }
 }
 
@@ -446,9 +450,12 @@ __global__ __launch_bounds__(1024) void giant_vote_kernel(u32* __restrict__ pare
 // per wave via ballot. giant_next receives g. Grid-stride in whole waves so the ballot covers 64 ids.
 __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__ parent, u32* __restrict__ labels, u32 n,
                                                                const u32* __restrict__ giant_prev,
-                                                               u32* __restrict__ giant_next, u64* __restrict__ bits) {
+                                                               u32* __restrict__ giant_next, u64* __restrict__ bits,
+                                                               u32* __restrict__ bloom_clear) {
     __shared__ u32 s_g;
     NoCount c;
+    if (bloom_clear)  // the bloom buffer the next fold records into (compress_inc_kernel)
+        for (u32 w = blockIdx.x * kBlock + threadIdx.x; w < gcc::kBloomBits / 32; w += gridDim.x * kBlock) bloom_clear[w] = 0;
     if (threadIdx.x == 0) {
         const u32 g0 = *giant_prev;
         s_g = (g0 == UNSEEN) ? UNSEEN : UF::find_from(parent, g0, parent[g0], c);
@@ -468,6 +475,82 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
         }
         const unsigned long long m = __ballot(g != UNSEEN && lab == g);
         if ((threadIdx.x & 63) == 0) bits[vv >> 6] = m;
+    }
+}
+
+// Incremental compress: parent[] was compressed at the last compress and every mutation since was recorded in
+// `bloom` (fold_kernel<true>; uf_device.h explains why an unmarked parent is still a root). labels[v] = p =
+// parent[v] unless p is marked, and only then a (read-only) find. So the pass is a coalesced stream of parent[]
+// and labels[] instead of a random read of parent[p] per seen non-root. One 1024-thread block per CU holds the
+// bloom in LDS; a lane reads 4 consecutive ids (16 B) and a wave covers 256 ids = 4 bitmap words of the
+// tracked component (as compress_bits_kernel). The block also clears its share of the other bloom buffer.
+constexpr int kIncBlock = 1024;
+typedef gcc::UnionFind<gcc::LoadPlain, false> UFRead;
+
+__device__ __forceinline__ u32 inc_label(const u32* parent, const u32* s_bloom, u32 v, u32 p) {
+    if (p >= v) return p;  // root (p == v) or UNSEEN
+    const u32 s = gcc::bloom_slot(p);
+    if (!((s_bloom[s >> 5] >> (s & 31)) & 1u)) return p;
+    NoCount c;
+    return UFRead::find_from(const_cast<u32*>(parent), v, p, c);
+}
+
+__global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* __restrict__ parent, u32* __restrict__ labels,
+                                                                 u32 n, const u32* __restrict__ bloom,
+                                                                 u32* __restrict__ bloom_clear,
+                                                                 const u32* __restrict__ giant_prev,
+                                                                 u32* __restrict__ giant_next, u64* __restrict__ bits) {
+    extern __shared__ __attribute__((aligned(16))) u32 s_bloom[];
+    __shared__ u32 s_g;
+    constexpr u32 kW4 = gcc::kBloomBits / 128;  // bloom size in 16-B words
+    {
+        const u32x4* src = reinterpret_cast<const u32x4*>(bloom);
+        u32x4* dst = reinterpret_cast<u32x4*>(s_bloom);
+        for (u32 w = threadIdx.x; w < kW4; w += kIncBlock) dst[w] = src[w];
+        const u32 per = (kW4 + gridDim.x - 1) / gridDim.x, a = blockIdx.x * per, b = min(kW4, a + per);
+        const u32x4 z = {0, 0, 0, 0};
+        for (u32 w = a + threadIdx.x; w < b; w += kIncBlock) reinterpret_cast<u32x4*>(bloom_clear)[w] = z;
+    }
+    if (threadIdx.x == 0) {
+        NoCount c;
+        const u32 g0 = *giant_prev;
+        s_g = (g0 == UNSEEN) ? UNSEEN : UFRead::find_from(const_cast<u32*>(parent), g0, parent[g0], c);
+        if (blockIdx.x == 0) *giant_next = s_g;
+    }
+    __syncthreads();
+    const u32 g = s_g;
+    const u32 lane = threadIdx.x & 63;
+    const u64 nwords = ((u64)n + 63) / 64;
+    const u64 nchunks = ((u64)n + 255) / 256;
+    const u64 nwaves = (u64)gridDim.x * (kIncBlock / 64);
+    for (u64 ch = (u64)blockIdx.x * (kIncBlock / 64) + (threadIdx.x >> 6); ch < nchunks; ch += nwaves) {
+        const u64 v0 = ch * 256 + 4 * lane;
+        u32 lab[4] = {UNSEEN, UNSEEN, UNSEEN, UNSEEN};
+        if (v0 + 3 < n) {
+            const u32x4 p = *reinterpret_cast<const u32x4*>(parent + v0);
+            lab[0] = inc_label(parent, s_bloom, (u32)v0, p.x);
+            lab[1] = inc_label(parent, s_bloom, (u32)v0 + 1, p.y);
+            lab[2] = inc_label(parent, s_bloom, (u32)v0 + 2, p.z);
+            lab[3] = inc_label(parent, s_bloom, (u32)v0 + 3, p.w);
+            const u32x4 o = {lab[0], lab[1], lab[2], lab[3]};
+            *reinterpret_cast<u32x4*>(labels + v0) = o;
+        } else {
+            for (u32 k = 0; k < 4; ++k)
+                if (v0 + k < n) {
+                    lab[k] = inc_label(parent, s_bloom, (u32)(v0 + k), parent[v0 + k]);
+                    labels[v0 + k] = lab[k];
+                }
+        }
+        u64 w = 0;
+        if (g != UNSEEN)
+            w = (u64)((lab[0] == g) | ((lab[1] == g) << 1) | ((lab[2] == g) << 2) | ((lab[3] == g) << 3))
+                << (4 * (lane & 15));
+        w |= __shfl_xor(w, 1, 64);
+        w |= __shfl_xor(w, 2, 64);
+        w |= __shfl_xor(w, 4, 64);
+        w |= __shfl_xor(w, 8, 64);
+        const u64 wi = ch * 4 + (lane >> 4);
+        if ((lane & 15) == 0 && wi < nwords) bits[wi] = w;
     }
 }
 
@@ -1025,6 +1108,11 @@ struct FoldTune {
     bool seed_nt = true;  // non-temporal loads in the BFS passes (false: the prefix may stay in the MALL)
     bool seed_global = false;  // also seed when the bitmap does not fit LDS (global-bitmap BFS lookups)
     bool seed_fuse = true;  // the first BFS pass elects the hub itself (no seed_hub launch, no flag clearing)
+    // incremental compress (compress_inc_kernel): plain folds record their mutations in a bloom filter when the
+    // forest spans >= inc_min_ids ids and a batch is at most 1/inc_div of them (a short window of a big forest)
+    bool incremental = true;
+    u64 inc_min_ids = 1ull << 22;
+    u64 inc_div = 8;
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -1056,6 +1144,12 @@ struct gcc_forest {
     u8* d_flags = nullptr;
     u32 flag_epoch = 0;  // the last epoch written into d_flags (0: needs clearing)
     u32* d_bmin = nullptr;  // seeding: per-block minima of the BFS passes (seed_pack_kernel<true> reduces them)
+    // incremental compress: two bloom buffers of gcc::kBloomBits bits. The folds record into d_bloom[bloom_cur];
+    // every compress clears the other one and flips. rec_all: every mutation since the last compress was recorded
+    u32* d_bloom = nullptr;
+    int bloom_cur = 0;
+    bool rec_all = false;
+    u32* bloom(int i) const { return d_bloom + (size_t)i * (gcc::kBloomBits / 32); }
 
     // pinned double-buffered staging for host-fed edges (per-edge foldEdges appends here)
     static constexpr u64 kStageEdges = 1ull << 20;  // 8 MiB per slot
@@ -1108,9 +1202,12 @@ int gcc_check_device(int device) {
     return GCC_OK;
 }
 
-static void mark_mutated(gcc_forest* h) {
+// recorded: the mutation was recorded in the bloom (or cleared rec_all itself); anything else rules out an
+// incremental compress until the next full one
+static void mark_mutated(gcc_forest* h, bool recorded = false) {
     h->host_valid = false;
     h->compressed = false;
+    if (!recorded) h->rec_all = false;
 }
 
 // Every kernel of the fold pipeline goes through launch_k. Timing mode launches it with hipExtLaunchKernelGGL's
@@ -1145,6 +1242,7 @@ static int launch_k(gcc_forest* h, const char* name, u64 edges, F kernel, dim3 g
 
 static int materialize_reset(gcc_forest* h) {
     if (!h->pending_reset) return GCC_OK;
+    h->rec_all = false;
     HIP_TRY(hipMemsetAsync(h->d_parent, 0xFF, (size_t)h->cap * sizeof(u32), h->stream));
     h->pending_reset = false;
     return GCC_OK;
@@ -1157,39 +1255,73 @@ static int alloc_filter(gcc_forest* h) {
     return GCC_OK;
 }
 
-// compress into the spare buffer and swap; with the filter on, refresh the giant bitmap from the new labels
+// incremental compresses are only worth their recording for big forests (the full compress of a few MiB is a
+// launch floor anyway); they also need 16-B aligned id-range buffers (the inc kernel's vector loads)
+static bool inc_forest(const gcc_forest* h) {
+    return h->tune.incremental && h->filter_enabled() && (u64)h->cap >= h->tune.inc_min_ids &&
+           ((reinterpret_cast<uintptr_t>(h->d_parent) | reinterpret_cast<uintptr_t>(h->d_spare)) & 15) == 0;
+}
+
+// compress into the spare buffer and swap; with the filter on, refresh the giant bitmap from the new labels.
+// Incremental (compress_inc_kernel) when every mutation since the last compress was recorded.
 static int compress_now(gcc_forest* h, const char* name = "compress") {
     int rc = GCC_OK;
+    const bool inc_here = inc_forest(h);
     if (!h->filter_enabled()) {
         rc = launch_k(h, name, 0, compress_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->d_parent,
                       h->d_spare, h->cap);
     } else {
         rc = alloc_filter(h);
         if (rc) return rc;
+        if (inc_here && !h->d_bloom) {
+            HIP_TRY(hipMalloc((void**)&h->d_bloom, 2 * (size_t)(gcc::kBloomBits / 8)));
+            HIP_TRY(hipMemsetAsync(h->d_bloom, 0, 2 * (size_t)(gcc::kBloomBits / 8), h->stream));
+            h->rec_all = false;
+        }
         if (!h->has_giant)  // first refresh of this forest: elect the component to track
             rc = launch_k(h, "vote", 0, giant_vote_kernel, dim3(1), dim3(1024), 0, h->d_parent, h->cap,
                           h->d_giant + h->giant_slot, h->d_giant + 4);
-        if (!rc)
+        u32* clear = h->d_bloom ? h->bloom(h->bloom_cur ^ 1) : nullptr;
+        if (!rc && inc_here && h->rec_all) {
+            static bool attr = false;
+            if (!attr) {
+                HIP_TRY(hipFuncSetAttribute((const void*)compress_inc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)(gcc::kBloomBits / 8)));
+                attr = true;
+            }
+            rc = launch_k(h, std::strcmp(name, "refresh") ? "compress_inc" : "refresh_inc", 0, compress_inc_kernel, dim3(h->n_cu), dim3(kIncBlock), gcc::kBloomBits / 8,
+                          (const u32*)h->d_parent, h->d_spare, h->cap, (const u32*)h->bloom(h->bloom_cur), clear,
+                          (const u32*)(h->d_giant + h->giant_slot), h->d_giant + (h->giant_slot ^ 1), h->d_bits);
+        } else if (!rc) {
             rc = launch_k(h, name, 0, compress_bits_kernel, dim3(grid_for(h->nwords() * 64ull, kMaxGrid)), dim3(kBlock), 0,
                           h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
-                          h->d_giant + (h->giant_slot ^ 1), h->d_bits);
+                          h->d_giant + (h->giant_slot ^ 1), h->d_bits, clear);
+        }
         h->giant_slot ^= 1;
         h->has_giant = true;
+        h->bloom_cur ^= 1;
     }
     if (rc) return rc;
     std::swap(h->d_parent, h->d_spare);
     h->compressed = true;
+    h->rec_all = inc_here && h->d_bloom;  // parent[] is compressed and the next fold's bloom is clear
     return GCC_OK;
 }
 
 static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* name) {
     if (n == 0) return GCC_OK;
-    return launch_k(h, name, n, fold_kernel, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent,
-                    reinterpret_cast<const u64*>(d_pairs), n);
+    const u64* edges = reinterpret_cast<const u64*>(d_pairs);
+    if (h->rec_all && n * std::max<u64>(1, h->tune.inc_div) <= (u64)h->cap)
+        return launch_k(h, name, n, fold_kernel<true>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent, edges,
+                        n, h->bloom(h->bloom_cur));
+    h->rec_all = false;
+    return launch_k(h, name, n, fold_kernel<false>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent, edges, n,
+                    (u32*)nullptr);
 }
 
 static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (n == 0) return GCC_OK;
+    h->rec_all = false;  // the filtered fold does not record its mutations
     const u32 nw = h->nwords() + (h->nwords() & 1);  // u64 bitmap words, rounded to 16 B
     const bool lds = nw <= kLdsBitmapMaxWords;
     const u32 nblocks = lds ? (u32)h->n_cu : kMaxGrid;
@@ -1253,6 +1385,7 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
 // prefix, parent[] := C ? gmin : UNSEEN. Replaces the reset memset; leaves has_giant set, bitmap = C.
 static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
     const FoldTune& t = h->tune;
+    h->rec_all = false;
     int rc = alloc_filter(h);
     if (rc) return rc;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
@@ -1420,7 +1553,7 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
         h->last_fold_first = ev_first;
         h->last_fold_last = (int)h->kev_used - 1;
     }
-    mark_mutated(h);
+    mark_mutated(h, true);  // the launches above cleared rec_all unless they recorded
     return GCC_OK;
 }
 
@@ -1616,6 +1749,7 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (h->d_scratch) (void)hipFree(h->d_scratch);
     if (h->d_witness) (void)hipFree(h->d_witness);
     if (h->d_bits) (void)hipFree(h->d_bits);
+    if (h->d_bloom) (void)hipFree(h->d_bloom);
     if (h->d_giant) (void)hipFree(h->d_giant);
     if (h->d_flags) (void)hipFree(h->d_flags);
     if (h->d_bmin) (void)hipFree(h->d_bmin);
@@ -1666,6 +1800,7 @@ int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent) {
     DeviceGuard g(h->device);
     int rc = flush(h);
     if (rc) return rc;
+    h->rec_all = false;  // the caller may write through the pointer: no incremental compress until a full one
     *d_parent = h->d_parent;
     return GCC_OK;
 }
@@ -1675,6 +1810,7 @@ int gcc_forest_reset(gcc_forest* h) {
     DeviceGuard g(h->device);
     h->staged = 0;
     h->pending_reset = true;  // materialised lazily (see gcc_forest::pending_reset)
+    h->rec_all = false;
     h->host_valid = false;
     h->compressed = true;  // all UNSEEN is canonical
     h->has_giant = false;  // the giant bitmap described the old forest
@@ -1788,6 +1924,7 @@ int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, u
     HIP_TRY(hipGetLastError());
     into->host_valid = false;
     into->compressed = false;
+    into->rec_all = false;
     return GCC_OK;
 }
 
@@ -1990,6 +2127,9 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "seed_refresh") t.seed_refresh = value;
     else if (k == "seed_fuse") t.seed_fuse = value != 0;
     else if (k == "filter_min_share") t.filter_min_share = value;
+    else if (k == "incremental") t.incremental = value != 0;
+    else if (k == "inc_min_ids") t.inc_min_ids = (u64)value;
+    else if (k == "inc_div") t.inc_div = std::max<u64>(1, (u64)value);
     else return set_err(GCC_E_INVALID, "unknown tuning key '%s'", key);
     return GCC_OK;
 }
@@ -2028,7 +2168,7 @@ int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size) {
         HIP_TRY(hipEventElapsedTime(&ms, h->kev[k.ev].first, h->kev[k.ev].second));
         snprintf(line, sizeof line, "%s %.5f %llu\n", k.name, ms, (unsigned long long)k.edges);
         out += line;
-        if (in_fold && std::strcmp(k.name, "compress") != 0) {  // kernels enqueued by this fold
+        if (in_fold && std::strcmp(k.name, "compress") != 0 && std::strcmp(k.name, "compress_inc") != 0) {  // this fold's
             if (first < 0) first = k.ev;
             last = k.ev;
             if (!std::strcmp(k.name, "filtered") || !std::strcmp(k.name, "plain") || !std::strcmp(k.name, "sample"))

@@ -45,6 +45,24 @@ struct Count {
     __device__ __forceinline__ void store() { ++n_store; }
 };
 
+// Mutation recorders for the incremental compress (gelly_cc.hip compress_inc_kernel). Between two compresses,
+// every id that LEAVES root state (a successful hook CAS) or leaves UNSEEN (makeSet, or a new id hung straight
+// under a root) is marked in a bloom filter of kBloomBits bits. Every parent value written during a window is an
+// id that was a root at some time of it (or at its start, when parent[] was compressed), so an id p that is not
+// marked and is some id's parent is still a root: that id's label is p, no find needed.
+constexpr u32 kBloomBits = 1u << 20;  // 128 KiB: one CU's LDS copy in the incremental compress
+__host__ __device__ __forceinline__ u32 bloom_slot(u32 x) { return (x * 0x9E3779B1u) >> 12; }
+struct NoRec {
+    __device__ __forceinline__ void mark(u32) const {}
+};
+struct BloomRec {
+    u32* bloom;
+    __device__ __forceinline__ void mark(u32 x) const {
+        const u32 s = bloom_slot(x);
+        atomicOr(&bloom[s >> 5], 1u << (s & 31));
+    }
+};
+
 template <class L, bool SPLIT, class C = NoCount>
 struct UnionFind {
     // makeSet-on-first-sight (DisjointSet.union :99-104): an observed parent of v that is not UNSEEN
@@ -80,12 +98,13 @@ struct UnionFind {
     // union (DisjointSet.union :97-123), min-id hooking with atomicCAS on the larger root.
     // An unseen endpoint v joining a component whose root r < v is made seen AND hung under r by ONE CAS
     // (UNSEEN -> r): the common case of a stream (a new vertex attaching to an existing component).
-    static __device__ __forceinline__ void unite(u32* parent, u32 u, u32 v, C& c) {
+    template <class R = NoRec>
+    static __device__ __forceinline__ void unite(u32* parent, u32 u, u32 v, C& c, const R& rec = R()) {
         u32 pu = L::ld(&parent[u]);
         if (u == v) {  // self loop: makeSet only
             if (pu == GCC_UNSEEN_DEV) {
                 c.cas();
-                atomicCAS(&parent[u], GCC_UNSEEN_DEV, u);
+                if (atomicCAS(&parent[u], GCC_UNSEEN_DEV, u) == GCC_UNSEEN_DEV) rec.mark(u);
             }
             return;
         }
@@ -99,6 +118,7 @@ struct UnionFind {
             const u32 lo = u < v ? u : v, hi = u < v ? v : u;
             c.cas();
             const u32 o = atomicCAS(&parent[lo], GCC_UNSEEN_DEV, lo);
+            if (o == GCC_UNSEEN_DEV) rec.mark(lo);
             u = lo;
             pu = (o == GCC_UNSEEN_DEV) ? lo : o;
             v = hi;
@@ -108,10 +128,14 @@ struct UnionFind {
             c.cas();
             if (ru < v) {
                 const u32 o = atomicCAS(&parent[v], GCC_UNSEEN_DEV, ru);
-                if (o == GCC_UNSEEN_DEV) return;  // v seen and hooked under ru in one step
+                if (o == GCC_UNSEEN_DEV) {  // v seen and hooked under ru in one step
+                    rec.mark(v);
+                    return;
+                }
                 pv = o;
             } else {
                 const u32 o = atomicCAS(&parent[v], GCC_UNSEEN_DEV, v);
+                if (o == GCC_UNSEEN_DEV) rec.mark(v);
                 pv = (o == GCC_UNSEEN_DEV) ? v : o;
             }
         }
@@ -121,11 +145,17 @@ struct UnionFind {
             const u32 hi = ru < rv ? rv : ru;
             c.cas();
             u32 old = atomicCAS(&parent[hi], hi, lo);
-            if (old == hi) return;
+            if (old == hi) {
+                rec.mark(hi);
+                return;
+            }
             c.cas_fail();
             if (old == GCC_UNSEEN_DEV) {  // unreachable for seen roots; keeps the loop finite regardless
                 old = atomicCAS(&parent[hi], GCC_UNSEEN_DEV, lo);
-                if (old == GCC_UNSEEN_DEV) return;
+                if (old == GCC_UNSEEN_DEV) {
+                    rec.mark(hi);
+                    return;
+                }
             }
             ru = find_from(parent, hi, old, c);
             rv = find_from(parent, lo, L::ld(&parent[lo]), c);
