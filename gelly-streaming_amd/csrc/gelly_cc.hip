@@ -89,6 +89,26 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(u32* __restrict__ parent, 
     }
 }
 
+// Global -> LDS copy of n 16-B words by a whole block: U loads in flight per thread before any store. A plain
+// `dst[w] = src[w]` loop waits for each load before it issues the next (measured: 6.7 us for a 128 KiB bitmap).
+template <int BLOCK>
+__device__ __forceinline__ void lds_fill(u32x4* dst, const u32x4* __restrict__ src, u32 n) {
+    constexpr int U = 8;
+    for (u32 base = 0; base < n; base += U * BLOCK) {
+        u32x4 r[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {  // unconditional (clamped) loads: the compiler can count them
+            const u32 w = base + k * BLOCK + threadIdx.x;
+            r[k] = src[w < n ? w : n - 1];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const u32 w = base + k * BLOCK + threadIdx.x;
+            if (w < n) dst[w] = r[k];
+        }
+    }
+}
+
 // Giant-filtered fold (Afforest-style skip): bits[] is a bitmap of one component C of the forest at some
 // earlier time (normally the largest). Components only grow, so an edge with both endpoints in C is already
 // folded in: it is skipped without touching parent[]. Every other edge is appended to the slow queue (or,
@@ -238,7 +258,7 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
     if constexpr (LDS) {
         const u32x4* src = reinterpret_cast<const u32x4*>(bits);
         u32x4* dst = reinterpret_cast<u32x4*>(s_dyn);
-        for (u32 w = threadIdx.x; w < nwords / 2; w += BLOCK) dst[w] = src[w];
+        if (nwords) lds_fill<BLOCK>(dst, src, nwords / 2);
         bm = s_dyn;
     }
     __syncthreads();
@@ -506,7 +526,7 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* __re
     {
         const u32x4* src = reinterpret_cast<const u32x4*>(bloom);
         u32x4* dst = reinterpret_cast<u32x4*>(s_bloom);
-        for (u32 w = threadIdx.x; w < kW4; w += kIncBlock) dst[w] = src[w];
+        lds_fill<kIncBlock>(dst, src, kW4);
         const u32 per = (kW4 + gridDim.x - 1) / gridDim.x, a = blockIdx.x * per, b = min(kW4, a + per);
         const u32x4 z = {0, 0, 0, 0};
         for (u32 w = a + threadIdx.x; w < b; w += kIncBlock) reinterpret_cast<u32x4*>(bloom_clear)[w] = z;
@@ -569,20 +589,21 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* __re
 //      skipped, every other edge (prefix included) takes the union path, so the result is exact.
 // ------------------------------------------------------------------------------------------------
 constexpr int kHubBlock = 1024;
-constexpr u32 kHubSlots = 4096;  // LDS open-addressing table (key, count): 32 KiB, load factor <= 1/2
+constexpr u32 kHubSlots = 16384;  // LDS open-addressing table (key, count): 128 KiB, load factor <= 1/8
 constexpr u32 kHubProbe = 64;
 constexpr u64 kHubSample = 1024;  // edges sampled for the hub vote (1 per thread)
 
-__device__ __forceinline__ void hub_count(u32 x, u32* s_key, u32* s_cnt) {
-    u32 s = (u32)(gcc_splitmix64(x) & (kHubSlots - 1));
+// Count one occurrence of x; returns x's count including this one (0 if the probe limit was hit). The thread
+// that makes the last increment of a key holds its final count, so the argmax needs no scan of the table.
+__device__ __forceinline__ u32 hub_count(u32 x, u32* s_key, u32* s_cnt) {
+    u32 s = (x * 0x9E3779B1u) >> (32 - 14);
+    static_assert(kHubSlots == (1u << 14), "hash width");
 #pragma unroll 1
     for (u32 p = 0; p < kHubProbe; ++p, s = (s + 1) & (kHubSlots - 1)) {
         const u32 k = atomicCAS(&s_key[s], UNSEEN, x);
-        if (k == UNSEEN || k == x) {
-            atomicAdd(&s_cnt[s], 1u);
-            return;
-        }
+        if (k == UNSEEN || k == x) return atomicAdd(&s_cnt[s], 1u) + 1;
     }
+    return 0;
 }
 
 __device__ __forceinline__ bool hub_better(u32 c, u32 k, u32 bc, u32 bk) { return c > bc || (c == bc && c && k < bk); }
@@ -610,26 +631,30 @@ __device__ __forceinline__ u32 hub_elect(const u64 (&e)[kHubPer], u32* s_tab) {
     constexpr int kPer = kHubPer;
     {
         const u32x4 kz = {UNSEEN, UNSEEN, UNSEEN, UNSEEN}, cz = {0, 0, 0, 0};
+#pragma unroll
         for (u32 s = threadIdx.x; s < kHubSlots / 4; s += kHubBlock) {
             reinterpret_cast<u32x4*>(s_key)[s] = kz;
             reinterpret_cast<u32x4*>(s_cnt)[s] = cz;
         }
     }
     __syncthreads();
+    // each thread keeps the best (count, key) among its own increments; argmax: count desc, id asc
+    u32 bc = 0, bk = UNSEEN;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         if (e[k] == ~0ull) continue;
-        hub_count((u32)e[k], s_key, s_cnt);
-        hub_count((u32)(e[k] >> 32), s_key, s_cnt);
-    }
-    __syncthreads();
-    // argmax over (count desc, id asc)
-    u32 bc = 0, bk = UNSEEN;
-    for (u32 s = threadIdx.x; s < kHubSlots; s += kHubBlock)
-        if (hub_better(s_cnt[s], s_key[s], bc, bk)) {
-            bc = s_cnt[s];
-            bk = s_key[s];
+        const u32 a = (u32)e[k], b = (u32)(e[k] >> 32);
+        const u32 ca = hub_count(a, s_key, s_cnt);
+        if (hub_better(ca, a, bc, bk)) {
+            bc = ca;
+            bk = a;
         }
+        const u32 cb = hub_count(b, s_key, s_cnt);
+        if (hub_better(cb, b, bc, bk)) {
+            bc = cb;
+            bk = b;
+        }
+    }
     for (int off = 32; off > 0; off >>= 1) {
         const u32 c2 = __shfl_down(bc, off, 64), k2 = __shfl_down(bk, off, 64);
         if (hub_better(c2, k2, bc, bk)) {
@@ -642,15 +667,19 @@ __device__ __forceinline__ u32 hub_elect(const u64 (&e)[kHubPer], u32* s_tab) {
         s_bk[threadIdx.x >> 6] = bk;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kHubBlock / 64; ++w)
-            if (hub_better(s_bc[w], s_bk[w], s_bc[0], s_bk[0])) {
-                s_bc[0] = s_bc[w];
-                s_bk[0] = s_bk[w];
-            }
+    // every wave reduces the kHubBlock / 64 wave winners itself (no serial loop, no further barrier)
+    const u32 lane = threadIdx.x & 63;
+    bc = lane < kHubBlock / 64 ? s_bc[lane] : 0;
+    bk = lane < kHubBlock / 64 ? s_bk[lane] : UNSEEN;
+    for (int off = 8; off > 0; off >>= 1) {
+        static_assert(kHubBlock / 64 == 16, "wave winners fit 16 lanes");
+        const u32 c2 = __shfl_xor(bc, off, 64), k2 = __shfl_xor(bk, off, 64);
+        if (hub_better(c2, k2, bc, bk)) {
+            bc = c2;
+            bk = k2;
+        }
     }
-    __syncthreads();
-    return s_bk[0];  // n_sample >= 1, so some endpoint was counted
+    return __shfl(bk, 0, 64);  // n_sample >= 1, so some endpoint was counted
 }
 
 // Elects h and initialises C = {h}: flags (zeroed up to a whole bitmap word) and the bitmap. Every block of
@@ -737,7 +766,7 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
     } else if constexpr (LDS) {
         const u32x4* src = reinterpret_cast<const u32x4*>(bits32);
         u32x4* dst = reinterpret_cast<u32x4*>(s_dyn);
-        for (u32 w = threadIdx.x; w < nwords32 / 4; w += BLOCK) dst[w] = src[w];
+        if (nwords32) lds_fill<BLOCK>(dst, src, nwords32 / 4);
         bm = s_dyn;
     }
     __syncthreads();
