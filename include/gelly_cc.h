@@ -168,8 +168,10 @@ int gcc_forest_last_fold_ms(gcc_forest* h, float* ms);
  * "phase ms edges" lines; each fold starts with a "begin" line (+ "slow_edges 0 n" lines in mode 2).
  * Recording never synchronises, so a timed region stays sync-free; this call synchronises. */
 int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size);
-/* fold-pipeline tuning knobs (filter, filter_min_batch, sample_first, sample_growth, sample_div,
- * refresh_min_batch, refresh1..refresh3); results never depend on them, only speed does */
+/* fold-pipeline tuning knobs; results never depend on them, only speed does. Keys: filter, filter_min_batch,
+ * filter_min_share, sample_first, sample_growth, sample_div, refresh_min_batch, refresh1..refresh3, depth, hook,
+ * drain_at, seed, seed_nt, seed_global, seed_fuse, seed_passes, seed_div, seed_div1, seed_refresh, incremental,
+ * inc_min_ids, inc_div. Unknown keys return GCC_E_INVALID. */
 int gcc_forest_tune(gcc_forest* h, const char* key, double value);
 
 #ifdef __cplusplus
