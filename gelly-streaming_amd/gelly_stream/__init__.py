@@ -6,6 +6,7 @@ Public surface mirrors the reference's operator API (`…/` = src/main/java/org/
   SummaryBulkAggregation   …/SummaryBulkAggregation.java      (window fold -> combine -> Merger)
   EdgesFold                …/EdgesFold.java
   SimpleEdgeStream         …/SimpleEdgeStream.java            (constructor + aggregate())
+  LongDisjointSet          DisjointSet<Long> for ids anywhere in the Long range (dense relabel, IdDictionary)
 All device work goes through libgelly_cc.so (include/gelly_cc.h); there is no CPU fallback.
 """
 from .aggregation import (EdgeBatch, EdgesFold, Merger, ReduceFunction, SummaryAggregation, SummaryBulkAggregation,
@@ -13,11 +14,13 @@ from .aggregation import (EdgeBatch, EdgesFold, Merger, ReduceFunction, SummaryA
 from .bipartite import BipartitenessCheck, Candidates, SignedVertex
 from .edgestream import SimpleEdgeStream
 from .library import CombineCC, ConnectedComponents, ConnectedComponentsTree, UpdateCC
+from .longids import IdDictionary, LongDisjointSet
 from .native import UNSEEN, GellyCCError, device_count
 from .summaries import DisjointSet
 
 __all__ = [
     "BipartitenessCheck", "Candidates", "CombineCC", "ConnectedComponents", "ConnectedComponentsTree", "DisjointSet",
-    "EdgeBatch", "EdgesFold", "GellyCCError", "Merger", "ReduceFunction", "SignedVertex", "SimpleEdgeStream",
-    "SummaryAggregation", "SummaryBulkAggregation", "SummaryTreeReduce", "UNSEEN", "UpdateCC", "device_count",
+    "EdgeBatch", "EdgesFold", "GellyCCError", "IdDictionary", "LongDisjointSet", "Merger", "ReduceFunction",
+    "SignedVertex", "SimpleEdgeStream", "SummaryAggregation", "SummaryBulkAggregation", "SummaryTreeReduce", "UNSEEN",
+    "UpdateCC", "device_count",
 ]

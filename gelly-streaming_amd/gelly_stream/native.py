@@ -90,6 +90,14 @@ _SIGS = {
     "gcc_forest_encode": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_forest_absorb": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_forest_absorb_many": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_uint64]),
+    # id dictionary for Java Long vertex ids (host-only)
+    "gcc_idmap_create": (c_int, [c_uint32, POINTER(c_void_p)]),
+    "gcc_idmap_destroy": (c_int, [c_void_p]),
+    "gcc_idmap_size": (c_int, [c_void_p, POINTER(c_uint64)]),
+    "gcc_idmap_map": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
+    "gcc_idmap_lookup": (c_int, [c_void_p, ctypes.c_int64, POINTER(c_uint32)]),
+    "gcc_idmap_ids": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_idmap_canonical": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, ctypes.c_int64]),
     # BipartitenessCheck's Candidates summary (signed forest)
     "gcc_signed_create": (c_int, [c_int, c_uint32, POINTER(c_void_p)]),
     "gcc_signed_destroy": (c_int, [c_void_p]),

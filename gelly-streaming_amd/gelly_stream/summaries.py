@@ -9,8 +9,8 @@ Differences a caller can observe (none affects the partition, which is the parit
   * roots are the MINIMUM vertex id of each component (min-id hooking), not union-by-rank roots, so
     ``find`` returns the canonical label and ``toString`` groups by min id;
   * ``getMatches()`` is a lazy read-only view: ``keys()`` are the vertices seen, ``get(v)`` the root;
-  * vertex ids are u32 in ``[0, id_capacity)`` (the Java K=Long ids of the benchmark fit; wider ids need a
-    dense relabel before the boundary — DESIGN.md §7).
+  * vertex ids are u32 in ``[0, id_capacity)`` (the Java K=Long ids of the benchmark fit; any other Long ids
+    go through LongDisjointSet, a dense relabel on the host side of the boundary — longids.py).
 """
 from __future__ import annotations
 

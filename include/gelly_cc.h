@@ -168,6 +168,22 @@ int gcc_forest_last_fold_ms(gcc_forest* h, float* ms);
  * "phase ms edges" lines; each fold starts with a "begin" line (+ "slow_edges 0 n" lines in mode 2).
  * Recording never synchronises, so a timed region stays sync-free; this call synchronises. */
 int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size);
+/* ---- id dictionary: Java Long vertex ids at the boundary (host-only, gelly_idmap.cpp) ----
+ * DisjointSet<Long> (…/summaries/DisjointSet.java:30-34) is keyed by any Long; the device forest by dense u32
+ * ids. The dictionary assigns dense ids in first-seen order and maps a forest's labels over dense ids back to
+ * the reference's canonical form: the minimum ORIGINAL id of the component (signed Long order). */
+typedef struct gcc_idmap gcc_idmap;
+int gcc_idmap_create(uint32_t capacity, gcc_idmap** out); /* at most `capacity` distinct ids */
+int gcc_idmap_destroy(gcc_idmap* m);
+int gcc_idmap_size(gcc_idmap* m, uint64_t* n_ids);
+/* dense_out[i] = dense id of ids[i] (a new id takes the next one); GCC_E_INVALID past the capacity */
+int gcc_idmap_map(gcc_idmap* m, const int64_t* ids, uint64_t n, uint32_t* dense_out);
+int gcc_idmap_lookup(gcc_idmap* m, int64_t id, uint32_t* dense); /* GCC_UNSEEN if never mapped */
+int gcc_idmap_ids(gcc_idmap* m, int64_t* out, uint64_t n);        /* out[d] = original id of dense id d */
+/* out[d] = min original id over d's component, for the first n dense ids; dense_labels = the forest's labels
+ * (gcc_forest_labels over the dense range); `unseen` is written for ids the forest has not seen */
+int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, int64_t* out, int64_t unseen);
+
 /* fold-pipeline tuning knobs; results never depend on them, only speed does. Keys: filter, filter_min_batch,
  * filter_min_share, sample_first, sample_growth, sample_div, refresh_min_batch, refresh1..refresh3, depth, hook,
  * drain_at, seed, seed_nt, seed_global, seed_fuse, seed_passes, seed_div, seed_div1, seed_refresh, incremental,

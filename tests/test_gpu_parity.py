@@ -457,3 +457,44 @@ def test_merge_message_full_c2_round_trip(torch_cuda):
     assert np.array_equal(c.labels(), la)
     for x in (a, b, c):
         x.close()
+
+
+# ---- DisjointSet<Long>: ids anywhere in the Long range (dense relabel at the boundary) ----
+def test_long_ids_connected_components_kat(golden):
+    """ConnectedComponentsTest's edges with every id mapped to a wide Long (negative and > 2^32): the same three
+    components, each labelled by its minimum wide id."""
+    from gelly_stream import LongDisjointSet
+
+    fx = golden("kat_connected_components.json")
+    wide = {v: (v - 5) * (1 << 40) + 3 for e in fx["edges"] for v in e}  # order-preserving, spans the sign
+    ds = LongDisjointSet(64)
+    ds.fold([[wide[a], wide[b]] for a, b in fx["edges"]])
+    comps = {}
+    for v, r in zip(*ds.seen_labels()):
+        comps.setdefault(int(r), []).append(int(v))
+    want = sorted(sorted(wide[v] for v in c) for c in fx["components"])
+    assert sorted(sorted(m) for m in comps.values()) == want
+    for c in fx["components"]:
+        assert ds.find(wide[c[-1]]) == min(wide[v] for v in c)
+    assert ds.find(12345) is None and ds.size() == len(wide) and ds.num_components() == 3
+    ds.close()
+
+
+def test_long_ids_random_stream_and_merge():
+    """A random stream over random 64-bit ids, folded in two halves into two summaries and merged (CombineCC),
+    against a union-find over the original ids."""
+    from gelly_stream import LongDisjointSet
+    from test_idmap import python_components
+
+    rng = np.random.default_rng(11)
+    universe = rng.integers(-(1 << 63), (1 << 63) - 1, size=50_000, dtype=np.int64)
+    pairs = universe[rng.integers(0, universe.size, size=(40_000, 2))]
+    want = python_components(pairs.tolist())
+    a, b = LongDisjointSet(1 << 17), LongDisjointSet(1 << 17)
+    a.fold(pairs[:20_000])
+    b.fold(pairs[20_000:])
+    a.merge(b)
+    ids, lab = a.seen_labels()
+    assert dict(zip(ids.tolist(), lab.tolist())) == want
+    a.close()
+    b.close()
