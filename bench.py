@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = min(16, cores))")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--tune", default="", help="fold-pipeline knobs k=v,... (gcc_forest_tune; speed only)")
     ap.add_argument("--phase-timing", choices=["timed", "after", "off"], default="after",
                     help="per-kernel dispatch events in the timed steps, in extra steps after them, or not at all")
     return ap.parse_args()
@@ -141,6 +142,8 @@ def main():
     stream = torch.cuda.current_stream(local)
     G.generate_device(cfg, rank * E1, E1, d_edges.data_ptr(), stream.cuda_stream)
     forest = TorchDisjointSet(V, local)
+    if args.tune:
+        forest.ds.tune(**{k: float(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
     group = ForestGroup() if world > 1 else None
     base_ptr = d_edges.data_ptr()
 
