@@ -1120,9 +1120,12 @@ struct FoldTune {
     u64 filter_min_batch = 1ull << 16;  // below this a fresh forest's batch is folded by fold_kernel alone
     u64 sample_first = 1ull << 12;      // first sampling launch; each next one is sample_growth x larger
     u64 sample_growth = 4;
-    u64 sample_div = 32;                // the sampling prefix is 1/sample_div of a fresh forest's first batch
+    u64 sample_div = 128;               // the sampling prefix is 1/sample_div of a fresh forest's first batch
+    u64 sample_min = 9ull << 15;        // ... and at least this many edges (C3: a shorter prefix left more CAS work)
     u64 refresh_min_batch = 1ull << 22; // batches above this refresh the giant bitmap at the refresh points
-    double refresh[3] = {1.0 / 4, 0, 0};  // refresh points (fractions of the batch), increasing, 0 = unused
+    // refresh points (fractions of the batch), increasing, 0 = unused. C4's per-GPU share: 5.37 -> 4.49 ms with
+    // a 1/128 sample and three early refreshes instead of 1/32 and one at 1/4 (profiles/r1_sweep_c4_refresh.log)
+    double refresh[3] = {0.04, 0.12, 0.30};
     bool filter = true;
     double filter_min_share = 0.5;  // the voted component must hold this share of the seen samples (0: no check)
     int depth = 4;  // 16-B edge-pair loads in flight per lane in the filtered kernel (4 or 8)
@@ -1540,7 +1543,7 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
         rc = launch_plain(h, d_pairs, n, "plain");
         b = n;
     } else if (!h->has_giant) {
-        const u64 s_end = std::min(n, std::max<u64>(t.filter_min_batch / 4, n / std::max<u64>(1, t.sample_div)));
+        const u64 s_end = std::min(n, std::max<u64>({t.filter_min_batch / 4, t.sample_min, n / std::max<u64>(1, t.sample_div)}));
         for (u64 c = std::max<u64>(1, t.sample_first); b < s_end && !rc; c *= std::max<u64>(2, t.sample_growth)) {
             const u64 e = std::min(s_end, b + c);
             rc = launch_plain(h, d_pairs + 2 * b, e - b, "sample");
@@ -2140,6 +2143,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "sample_first") t.sample_first = (u64)value;
     else if (k == "sample_growth") t.sample_growth = (u64)value;
     else if (k == "sample_div") t.sample_div = (u64)value;
+    else if (k == "sample_min") t.sample_min = (u64)value;
     else if (k == "refresh_min_batch") t.refresh_min_batch = (u64)value;
     else if (k == "refresh1") t.refresh[0] = value;
     else if (k == "refresh2") t.refresh[1] = value;

@@ -185,7 +185,7 @@ int gcc_idmap_ids(gcc_idmap* m, int64_t* out, uint64_t n);        /* out[d] = or
 int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, int64_t* out, int64_t unseen);
 
 /* fold-pipeline tuning knobs; results never depend on them, only speed does. Keys: filter, filter_min_batch,
- * filter_min_share, sample_first, sample_growth, sample_div, refresh_min_batch, refresh1..refresh3, depth, hook,
+ * filter_min_share, sample_first, sample_growth, sample_div, sample_min, refresh_min_batch, refresh1..refresh3, depth, hook,
  * drain_at, seed, seed_nt, seed_global, seed_fuse, seed_passes, seed_div, seed_div1, seed_refresh, incremental,
  * inc_min_ids, inc_div. Unknown keys return GCC_E_INVALID. */
 int gcc_forest_tune(gcc_forest* h, const char* key, double value);
