@@ -206,7 +206,7 @@ def main():
     # per-kernel durations (each kernel's own dispatch events) and per-fold device spans, grouped by kernel
     kernel_of = {"filtered": "fold_filtered_kernel", "sample": "fold_kernel", "plain": "fold_kernel",
                  "seed_hub": "seed_hub_kernel", "seed_bfs": "seed_bfs_kernel", "seed_pack": "seed_pack_kernel",
-                 "seed_init": "seed_pack_kernel", "refresh": "compress_bits_kernel", "compress": "compress_bits_kernel",
+                 "seed_init": "seed_pack_kernel", "refresh": "compress_bits_kernel", "compress": "compress_bits_kernel", "refresh_bits": "compress_bits_kernel",
                  "compress_inc": "compress_inc_kernel", "refresh_inc": "compress_inc_kernel",
                  "vote": "giant_vote_kernel"}
     phases, kernels, spans = {}, {}, []

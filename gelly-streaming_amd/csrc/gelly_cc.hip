@@ -491,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
             const u32 v = (u32)vv;
             const u32 p = parent[v];
             lab = (p >= v) ? p : UF::find_from(parent, v, p, c);
-            labels[v] = lab;
+            if (labels) labels[v] = lab;  // null: a mid-fold refresh of the bitmap alone (refresh_now)
         }
         const unsigned long long m = __ballot(g != UNSEEN && lab == g);
         if ((threadIdx.x & 63) == 0) bits[vv >> 6] = m;
@@ -1142,6 +1142,7 @@ struct FoldTune {
     bool seed_fuse = true;  // the first BFS pass elects the hub itself (no seed_hub launch, no flag clearing)
     // incremental compress (compress_inc_kernel): plain folds record their mutations in a bloom filter when the
     // forest spans >= inc_min_ids ids and a batch is at most 1/inc_div of them (a short window of a big forest)
+    bool refresh_labels = false;  // mid-fold refreshes: bitmap only (false) or a full compress (true)
     bool incremental = true;
     u64 inc_min_ids = 1ull << 22;
     u64 inc_div = 8;
@@ -1337,6 +1338,26 @@ static int compress_now(gcc_forest* h, const char* name = "compress") {
     std::swap(h->d_parent, h->d_spare);
     h->compressed = true;
     h->rec_all = inc_here && h->d_bloom;  // parent[] is compressed and the next fold's bloom is clear
+    return GCC_OK;
+}
+
+// Mid-fold refresh of the tracked component's bitmap (and its root) without a compress: the filter only needs
+// the bitmap, and writing 4 B of labels per id (then swapping buffers) doubles the pass's traffic. Path
+// splitting in the finds still shortens the forest. tune.refresh_labels = 1: a full compress instead.
+static int refresh_now(gcc_forest* h) {
+    if (h->tune.refresh_labels || !h->filter_enabled()) return compress_now(h, "refresh");
+    int rc = alloc_filter(h);
+    if (rc) return rc;
+    if (!h->has_giant)
+        rc = launch_k(h, "vote", 0, giant_vote_kernel, dim3(1), dim3(1024), 0, h->d_parent, h->cap,
+                      h->d_giant + h->giant_slot, h->d_giant + 4);
+    if (!rc)
+        rc = launch_k(h, "refresh_bits", 0, compress_bits_kernel, dim3(grid_for(h->nwords() * 64ull, kMaxGrid)),
+                      dim3(kBlock), 0, h->d_parent, (u32*)nullptr, h->cap, (const u32*)(h->d_giant + h->giant_slot),
+                      h->d_giant + (h->giant_slot ^ 1), h->d_bits, (u32*)nullptr);
+    if (rc) return rc;
+    h->giant_slot ^= 1;
+    h->has_giant = true;
     return GCC_OK;
 }
 
@@ -1543,13 +1564,16 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
         rc = launch_plain(h, d_pairs, n, "plain");
         b = n;
     } else if (!h->has_giant) {
-        const u64 s_end = std::min(n, std::max<u64>({t.filter_min_batch / 4, t.sample_min, n / std::max<u64>(1, t.sample_div)}));
+        // 1/sample_div of the batch, but at least min(sample_min, 1/32 of it): a short batch (a C5 window) keeps
+        // a sample well below its length, so the vote-share check below still runs
+        const u64 s_end = std::min(n, std::max<u64>({t.filter_min_batch / 4, n / std::max<u64>(1, t.sample_div),
+                                                     std::min<u64>(t.sample_min, n / 32)}));
         for (u64 c = std::max<u64>(1, t.sample_first); b < s_end && !rc; c *= std::max<u64>(2, t.sample_growth)) {
             const u64 e = std::min(s_end, b + c);
             rc = launch_plain(h, d_pairs + 2 * b, e - b, "sample");
             b = e;
         }
-        if (!rc && b < n) rc = compress_now(h, "refresh");
+        if (!rc && b < n) rc = refresh_now(h);
         if (!rc && b < n && t.filter_min_share > 0) {
             // once per forest: is the voted component a giant among the seen samples? If not, the filter would
             // send almost every edge down its slow path, and the plain fold is faster (C3, C5)
@@ -1576,7 +1600,7 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
         rc = launch_filtered(h, d_pairs + 2 * b, e - b);
         b = e;
         if (!rc && b < n) {
-            rc = compress_now(h, "refresh");
+            rc = refresh_now(h);
             ++next_refresh;
         }
     }
@@ -2161,6 +2185,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "seed_fuse") t.seed_fuse = value != 0;
     else if (k == "filter_min_share") t.filter_min_share = value;
     else if (k == "incremental") t.incremental = value != 0;
+    else if (k == "refresh_labels") t.refresh_labels = value != 0;
     else if (k == "inc_min_ids") t.inc_min_ids = (u64)value;
     else if (k == "inc_div") t.inc_div = std::max<u64>(1, (u64)value);
     else return set_err(GCC_E_INVALID, "unknown tuning key '%s'", key);
