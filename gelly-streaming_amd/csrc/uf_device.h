@@ -45,11 +45,13 @@ struct Count {
     __device__ __forceinline__ void store() { ++n_store; }
 };
 
-// Mutation recorders for the incremental compress (gelly_cc.hip compress_inc_kernel). Between two compresses,
-// every id that LEAVES root state (a successful hook CAS) or leaves UNSEEN (makeSet, or a new id hung straight
-// under a root) is marked in a bloom filter of kBloomBits bits. Every parent value written during a window is an
-// id that was a root at some time of it (or at its start, when parent[] was compressed), so an id p that is not
-// marked and is some id's parent is still a root: that id's label is p, no find needed.
+// Mutation recorder for the incremental compress (gelly_cc.hip compress_inc_kernel). Between two compresses,
+// every id that LEAVES root state (a successful hook CAS) is marked in a bloom filter of kBloomBits bits. Every
+// parent value is an id that was a root at some time since the last compress (parent[] was compressed then, and
+// every value written since is a root returned by find, or a copy of a parent value in path splitting; a stale
+// UNSEEN read only stops a find at an id reached through a parent pointer, so at such an id). So an unmarked id
+// p that is some id's parent is still a root: that id's label is p, no find needed. Ids that leave UNSEEN need
+// no mark: one hung straight under a root never becomes a parent value, one made a root is marked if hooked.
 constexpr u32 kBloomBits = 1u << 20;  // 128 KiB: one CU's LDS copy in the incremental compress
 __host__ __device__ __forceinline__ u32 bloom_slot(u32 x) { return (x * 0x9E3779B1u) >> 12; }
 struct NoRec {
@@ -104,7 +106,7 @@ struct UnionFind {
         if (u == v) {  // self loop: makeSet only
             if (pu == GCC_UNSEEN_DEV) {
                 c.cas();
-                if (atomicCAS(&parent[u], GCC_UNSEEN_DEV, u) == GCC_UNSEEN_DEV) rec.mark(u);
+                atomicCAS(&parent[u], GCC_UNSEEN_DEV, u);
             }
             return;
         }
@@ -118,7 +120,6 @@ struct UnionFind {
             const u32 lo = u < v ? u : v, hi = u < v ? v : u;
             c.cas();
             const u32 o = atomicCAS(&parent[lo], GCC_UNSEEN_DEV, lo);
-            if (o == GCC_UNSEEN_DEV) rec.mark(lo);
             u = lo;
             pu = (o == GCC_UNSEEN_DEV) ? lo : o;
             v = hi;
@@ -128,14 +129,10 @@ struct UnionFind {
             c.cas();
             if (ru < v) {
                 const u32 o = atomicCAS(&parent[v], GCC_UNSEEN_DEV, ru);
-                if (o == GCC_UNSEEN_DEV) {  // v seen and hooked under ru in one step
-                    rec.mark(v);
-                    return;
-                }
+                if (o == GCC_UNSEEN_DEV) return;  // v seen and hooked under ru in one step
                 pv = o;
             } else {
                 const u32 o = atomicCAS(&parent[v], GCC_UNSEEN_DEV, v);
-                if (o == GCC_UNSEEN_DEV) rec.mark(v);
                 pv = (o == GCC_UNSEEN_DEV) ? v : o;
             }
         }
