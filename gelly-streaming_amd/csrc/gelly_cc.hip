@@ -515,7 +515,13 @@ __device__ __forceinline__ u32 inc_label(const u32* parent, const u32* s_bloom, 
     return UFRead::find_from(const_cast<u32*>(parent), v, p, c);
 }
 
-__global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* __restrict__ parent, u32* __restrict__ labels,
+// INPLACE: labels == parent. parent[] is already canonical except where a marked parent needs the find, so only
+// those slots are written (with the root; each slot by its own lane only). That is race-free: the finds are
+// read-only, no root moves during a compress, and a lane that reads a slot before or after its owner rewrites it
+// gets an ancestor either way (the old parent or the root). The pass then reads parent[] and writes only the
+// changed slots instead of streaming a second 4 B per id into the spare buffer.
+template <bool INPLACE>
+__global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* parent, u32* labels,
                                                                  u32 n, const u32* __restrict__ bloom,
                                                                  u32* __restrict__ bloom_clear,
                                                                  const u32* __restrict__ giant_prev,
@@ -543,6 +549,8 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* __re
     const u64 nwords = ((u64)n + 63) / 64;
     const u64 nchunks = ((u64)n + 255) / 256;
     const u64 nwaves = (u64)gridDim.x * (kIncBlock / 64);
+    // (a 4-chunk software pipeline of the parent[] loads measured slower on C5: the finds of relabelled ids,
+    // not the stream, bound this pass there; profiles/r1_sweep_inc_inplace.log)
     for (u64 ch = (u64)blockIdx.x * (kIncBlock / 64) + (threadIdx.x >> 6); ch < nchunks; ch += nwaves) {
         const u64 v0 = ch * 256 + 4 * lane;
         u32 lab[4] = {UNSEEN, UNSEEN, UNSEEN, UNSEEN};
@@ -552,13 +560,21 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* __re
             lab[1] = inc_label(parent, s_bloom, (u32)v0 + 1, p.y);
             lab[2] = inc_label(parent, s_bloom, (u32)v0 + 2, p.z);
             lab[3] = inc_label(parent, s_bloom, (u32)v0 + 3, p.w);
-            const u32x4 o = {lab[0], lab[1], lab[2], lab[3]};
-            *reinterpret_cast<u32x4*>(labels + v0) = o;
+            if constexpr (INPLACE) {
+                if (lab[0] != p.x) labels[v0] = lab[0];
+                if (lab[1] != p.y) labels[v0 + 1] = lab[1];
+                if (lab[2] != p.z) labels[v0 + 2] = lab[2];
+                if (lab[3] != p.w) labels[v0 + 3] = lab[3];
+            } else {
+                const u32x4 o = {lab[0], lab[1], lab[2], lab[3]};
+                *reinterpret_cast<u32x4*>(labels + v0) = o;
+            }
         } else {
             for (u32 k = 0; k < 4; ++k)
                 if (v0 + k < n) {
-                    lab[k] = inc_label(parent, s_bloom, (u32)(v0 + k), parent[v0 + k]);
-                    labels[v0 + k] = lab[k];
+                    const u32 pk = parent[v0 + k];
+                    lab[k] = inc_label(parent, s_bloom, (u32)(v0 + k), pk);
+                    if (!INPLACE || lab[k] != pk) labels[v0 + k] = lab[k];
                 }
         }
         u64 w = 0;
@@ -1144,6 +1160,7 @@ struct FoldTune {
     // forest spans >= inc_min_ids ids and a batch is at most 1/inc_div of them (a short window of a big forest)
     bool refresh_labels = false;  // mid-fold refreshes: bitmap only (false) or a full compress (true)
     bool incremental = true;
+    bool inc_inplace = true;  // the incremental compress rewrites only changed parent[] slots (no spare buffer)
     u64 inc_min_ids = 1ull << 22;
     u64 inc_div = 8;
 };
@@ -1299,6 +1316,7 @@ static bool inc_forest(const gcc_forest* h) {
 // Incremental (compress_inc_kernel) when every mutation since the last compress was recorded.
 static int compress_now(gcc_forest* h, const char* name = "compress") {
     int rc = GCC_OK;
+    bool inplace = false;  // the compress rewrote d_parent itself (no swap)
     const bool inc_here = inc_forest(h);
     if (!h->filter_enabled()) {
         rc = launch_k(h, name, 0, compress_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->d_parent,
@@ -1318,13 +1336,20 @@ static int compress_now(gcc_forest* h, const char* name = "compress") {
         if (!rc && inc_here && h->rec_all) {
             static bool attr = false;
             if (!attr) {
-                HIP_TRY(hipFuncSetAttribute((const void*)compress_inc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)(gcc::kBloomBits / 8)));
+                for (const void* f : {(const void*)compress_inc_kernel<false>, (const void*)compress_inc_kernel<true>})
+                    HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(gcc::kBloomBits / 8)));
                 attr = true;
             }
-            rc = launch_k(h, std::strcmp(name, "refresh") ? "compress_inc" : "refresh_inc", 0, compress_inc_kernel, dim3(h->n_cu), dim3(kIncBlock), gcc::kBloomBits / 8,
-                          (const u32*)h->d_parent, h->d_spare, h->cap, (const u32*)h->bloom(h->bloom_cur), clear,
-                          (const u32*)(h->d_giant + h->giant_slot), h->d_giant + (h->giant_slot ^ 1), h->d_bits);
+            const char* kname = std::strcmp(name, "refresh") ? "compress_inc" : "refresh_inc";
+            inplace = h->tune.inc_inplace;
+            rc = inplace ? launch_k(h, kname, 0, compress_inc_kernel<true>, dim3(h->n_cu), dim3(kIncBlock),
+                                    gcc::kBloomBits / 8, (const u32*)h->d_parent, h->d_parent, h->cap,
+                                    (const u32*)h->bloom(h->bloom_cur), clear, (const u32*)(h->d_giant + h->giant_slot),
+                                    h->d_giant + (h->giant_slot ^ 1), h->d_bits)
+                         : launch_k(h, kname, 0, compress_inc_kernel<false>, dim3(h->n_cu), dim3(kIncBlock),
+                                    gcc::kBloomBits / 8, (const u32*)h->d_parent, h->d_spare, h->cap,
+                                    (const u32*)h->bloom(h->bloom_cur), clear, (const u32*)(h->d_giant + h->giant_slot),
+                                    h->d_giant + (h->giant_slot ^ 1), h->d_bits);
         } else if (!rc) {
             rc = launch_k(h, name, 0, compress_bits_kernel, dim3(grid_for(h->nwords() * 64ull, kMaxGrid)), dim3(kBlock), 0,
                           h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
@@ -1335,7 +1360,7 @@ static int compress_now(gcc_forest* h, const char* name = "compress") {
         h->bloom_cur ^= 1;
     }
     if (rc) return rc;
-    std::swap(h->d_parent, h->d_spare);
+    if (!inplace) std::swap(h->d_parent, h->d_spare);
     h->compressed = true;
     h->rec_all = inc_here && h->d_bloom;  // parent[] is compressed and the next fold's bloom is clear
     return GCC_OK;
@@ -2185,6 +2210,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "seed_fuse") t.seed_fuse = value != 0;
     else if (k == "filter_min_share") t.filter_min_share = value;
     else if (k == "incremental") t.incremental = value != 0;
+    else if (k == "inc_inplace") t.inc_inplace = value != 0;
     else if (k == "refresh_labels") t.refresh_labels = value != 0;
     else if (k == "inc_min_ids") t.inc_min_ids = (u64)value;
     else if (k == "inc_div") t.inc_div = std::max<u64>(1, (u64)value);

@@ -187,7 +187,7 @@ int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, 
 /* fold-pipeline tuning knobs; results never depend on them, only speed does. Keys: filter, filter_min_batch,
  * filter_min_share, sample_first, sample_growth, sample_div, sample_min, refresh_min_batch, refresh1..refresh3, depth, hook,
  * drain_at, seed, seed_nt, seed_global, seed_fuse, seed_passes, seed_div, seed_div1, seed_refresh, incremental,
- * inc_min_ids, inc_div, refresh_labels. Unknown keys return GCC_E_INVALID. */
+ * inc_min_ids, inc_div, inc_inplace, refresh_labels. Unknown keys return GCC_E_INVALID. */
 int gcc_forest_tune(gcc_forest* h, const char* key, double value);
 
 #ifdef __cplusplus

@@ -224,21 +224,23 @@ def test_adversarial_full_stream_closed_form(torch_cuda):
 def test_incremental_compress_windows(torch_cuda):
     """Short windows over a big forest: the plain folds record their mutations in a bloom filter and every window's
     compress is incremental (compress_inc_kernel). G(n, m) at the percolation threshold (n = 2^22, m = 2^21, deep
-    chains), 32 windows of 2^16 edges: every window equals the oracle and a forest with the incremental compress
-    off. A CombineCC merge, the raw-pointer view and a reset in between force full compresses."""
+    chains), 32 windows of 2^16 edges: every window equals the oracle, a forest with the incremental compress
+    off and one whose incremental compress writes a spare buffer instead of parent[] in place (inc_inplace=0).
+    A CombineCC merge, the raw-pointer view and a reset in between force full compresses."""
     cfg = G.scaled(G.CONFIGS["c3_gnm24"], n_vertices=1 << 22, n_edges=1 << 21, seed=0x1234)
     E, V = cfg.info()
     W = 1 << 16
     starts = np.arange(0, E + 1, W, dtype=np.uint64)
     want = orc.cc_stream(G.generate_host(cfg), starts, V, partitions=2, threads=2)
     d = device_stream(torch_cuda, cfg)
-    inc, full = DisjointSet(V), DisjointSet(V)
+    inc, full, spare = DisjointSet(V), DisjointSet(V), DisjointSet(V)
     full.tune(incremental=0)
+    spare.tune(inc_inplace=0)
     side = DisjointSet(V)  # a partial forest merged into `inc` mid-stream (CombineCC)
     side.fold_device(d.data_ptr(), W)
     for w in range(len(starts) - 1):
         b, e = int(starts[w]), int(starts[w + 1])
-        for ds in (inc, full):
+        for ds in (inc, full, spare):
             ds.fold_device(d.data_ptr() + 8 * b, e - b)
         if w == 9:
             inc.merge(side)  # edges of window 0 again: the partition is unchanged, the next compress is full
@@ -246,13 +248,14 @@ def test_incremental_compress_windows(torch_cuda):
             inc.device_ptr()
         got = inc.labels()
         assert np.array_equal(got, full.labels()), (w, first_mismatch(got, full.labels()))
+        assert np.array_equal(spare.labels(), full.labels()), ("inc_inplace=0", w)
         assert orc.label_digest(got) == int(want["digest"][w]), w
     # reset, then the same windows again from scratch
     inc.reset()
     for w in range(4):
         inc.fold_device(d.data_ptr() + 8 * int(starts[w]), W)
         assert orc.label_digest(inc.labels()) == int(want["digest"][w]), ("after reset", w)
-    for ds in (inc, full, side):
+    for ds in (inc, full, spare, side):
         ds.close()
 
 
