@@ -4,6 +4,7 @@ Canonical form (the parity contract): after every merge window
 component over all edges folded so far, 0xFFFFFFFF for ids never seen. Run with: pytest -m gpu
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -14,6 +15,7 @@ from gelly_stream import generators as G
 
 pytestmark = pytest.mark.gpu
 UNSEEN = 0xFFFFFFFF
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -501,3 +503,60 @@ def test_long_ids_random_stream_and_merge():
     assert dict(zip(ids.tolist(), lab.tolist())) == want
     a.close()
     b.close()
+
+
+# ---- every tuning knob leaves the result unchanged ----
+# One non-default setting per key that include/gelly_cc.h lists (gcc_forest_tune), chosen so that the path it
+# selects actually runs at this size (e.g. inc_min_ids low enough for the incremental compress to engage).
+KNOB_CASES = {
+    "filter": {"filter": 0}, "filter_min_batch": {"filter_min_batch": 1024},
+    "filter_min_share": {"filter_min_share": 0}, "sample_first": {"sample_first": 1024},
+    "sample_growth": {"sample_growth": 2}, "sample_div": {"sample_div": 8}, "sample_min": {"sample_min": 4096},
+    "refresh_min_batch": {"refresh_min_batch": 1024}, "refresh1": {"refresh_min_batch": 1024, "refresh1": 0.1},
+    "refresh2": {"refresh_min_batch": 1024, "refresh2": 0.2}, "refresh3": {"refresh_min_batch": 1024, "refresh3": 0.6},
+    "depth": {"depth": 8}, "hook": {"hook": 0}, "drain_at": {"drain_at": 1}, "seed": {"seed": 0},
+    "seed_nt": {"seed_nt": 0}, "seed_global": {"seed_global": 1}, "seed_fuse": {"seed_fuse": 0},
+    "seed_passes": {"seed_passes": 3}, "seed_div": {"seed_div": 2}, "seed_div1": {"seed_div1": 5},
+    "seed_refresh": {"seed_refresh": 0.5}, "incremental": {"inc_min_ids": 1024, "incremental": 0},
+    "inc_min_ids": {"inc_min_ids": 1024}, "inc_div": {"inc_min_ids": 1024, "inc_div": 1},
+    "inc_inplace": {"inc_min_ids": 1024, "inc_inplace": 0},
+    "refresh_labels": {"refresh_min_batch": 1024, "refresh_labels": 1},
+}
+
+
+def header_tuning_keys():
+    text = open(os.path.join(ROOT, "include", "gelly_cc.h")).read()
+    block = text[text.index("tuning knobs"):text.index("int gcc_forest_tune")]
+    block = block[block.index("Keys:") + 5:block.index("Unknown keys")]
+    keys = []
+    for part in block.replace("*", " ").replace("\n", " ").split(","):
+        part = part.strip().rstrip(".")
+        if part.startswith("refresh1..refresh"):
+            keys += ["refresh1", "refresh2", "refresh3"]
+        elif part:
+            keys.append(part)
+    return keys
+
+
+def test_every_tuning_knob_is_bit_exact(torch_cuda):
+    """Results never depend on the tuning (gelly_cc.h). Each key the header lists, set away from its default,
+    folds an R-MAT stream (one long window, then short windows over the same forest) bit-exactly; an unknown
+    key is rejected with GCC_E_INVALID."""
+    keys = header_tuning_keys()
+    assert sorted(keys) == sorted(KNOB_CASES), "a tuning key without a parity case (or a stale one)"
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=16, n_edges=1 << 20, seed=0x6B6E6F62)
+    E, V = cfg.info()
+    h = 1 << 19
+    starts = np.array([0, h, h + 4096, h + 8192, h + 12288, E], dtype=np.uint64)
+    want = orc.cc_stream(G.generate_host(cfg), starts, V, partitions=2, threads=2)["digest"]
+    d = device_stream(torch_cuda, cfg)
+    with DisjointSet(V) as ds:
+        with pytest.raises(GellyCCError):
+            ds.tune(no_such_knob=1)
+    for key, knobs in KNOB_CASES.items():
+        with DisjointSet(V) as ds:
+            ds.tune(**knobs)
+            for w in range(len(starts) - 1):
+                b, e = int(starts[w]), int(starts[w + 1])
+                ds.fold_device(d.data_ptr() + 8 * b, e - b)
+                assert orc.label_digest(ds.labels()) == int(want[w]), (key, w)
