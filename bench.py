@@ -1,20 +1,27 @@
 #!/usr/bin/env python3
 """Benchmark: edges/sec into the streaming connected-components summary on MI355X (BASELINE.json metric).
 
-One step = one pass of the hot path over one batch of synthetic input: reset the summary to its initial
-value, fold this rank's edge chunk (already resident in HBM) window by window into the device forest,
-and emit the summary after every window (canonicalising compress; with N>1 the butterfly forest merge
-over RCCL/xGMI first). Weak scaling: every rank folds the same number of edges of one shared stream
-(rank r owns chunk r), so value = N * edges_per_rank * K / max-over-ranks time.
+One step = one pass of the hot path over one synthetic stream already resident in HBM: reset the summary to its
+initial value, then per merge window fold this rank's chunk of the window into the device forest and emit the
+summary (canonicalising compress; with N > 1 the cross-GPU forest merge over RCCL/xGMI first).
 
-N=1 default workload: configs[1] = R-MAT scale 20 (1M vertices, 16M edges), one merge window per step.
+Partitioning (the reference's: SummaryBulkAggregation.java:93-106 tags each edge with an arbitrary upstream
+subtask, so a partition is any split of each window): every workload is ONE fixed stream, and rank r of N folds the
+r-th contiguous 1/N of every window. Strong scaling: value = (edges of the whole stream) * K / max-over-ranks time.
+
+N=1 default workload: C4, Kronecker scale 26 (64M vertices, 2^30 edges, 8 GiB of edges), one merge window — the
+config the north-star target is quoted on; it fits one GPU. Extra legs on rank 0 at N=1 (outside the timed
+region of the headline value): host-fed rate (pinned host memory + H2D), C2 R-MAT s20 rotating over 4 distinct
+batches (537 MB: no batch is still in the 256 MiB Infinity Cache when it is folded again), CPU baseline (the C
+restatement of the reference topology, oracle/cc_oracle.c) at T = 1, the box's CPU quota and nproc threads.
+Parity: the final labels' digest vs tests/golden/stream_digests.json (oracle digests computed on the CPU).
+
 Launch: python bench.py [--gpus N --steps K --warmup W]  (N>1 under torch.distributed.run, one rank per GPU).
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -33,33 +40,66 @@ KERNEL_BYTES = {
     "compress_inc_kernel": (8.125, "id"),   # the same, incremental (bloom of the window's mutations in LDS)
     "seed_pack_kernel": (5.125, "id"),      # flag byte read + parent write + 1 bitmap bit (the init variant)
     "seed_hub_kernel": (1.125, "id"),       # flag byte + bitmap bit cleared
+    "bucket_kernel": (16, "edge"),          # read the edge + write it into its u-slice bucket
+    "slice_filter_kernel": (12, "edge"),    # read the bucketed edge + write v of u-in-giant edges (4 B)
+    "slice_hook_kernel": (4, "edge"),       # read the v list
+    "bucket_init_kernel": (4.125, "id"),    # parent write + 1 bitmap bit
 }
+C2_BATCHES = 4  # rotating C2 batches (tests/golden/stream_digests.json c2_rmat20@k)
+HOST_FED_MAX_EDGES = 1 << 28  # the host-fed leg's sample (2 GiB of pinned host edges)
+CPU_SAMPLE_EDGES = 1 << 24    # the CPU baseline's sample (a prefix of the workload's stream)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2_rmat20")
-    ap.add_argument("--window-edges", type=int, default=0, help="edges per merge window per rank (0 = config default)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU-baseline threads (0 = min(16, cores))")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c4_kron26")
+    ap.add_argument("--window-edges", type=int, default=0, help="edges per merge window (0 = config default)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target CPU-baseline work per thread count (0 = skip)")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the host-fed and rotating-C2 legs")
     ap.add_argument("--tune", default="", help="fold-pipeline knobs k=v,... (gcc_forest_tune; speed only)")
     ap.add_argument("--phase-timing", choices=["timed", "after", "off"], default="after",
                     help="per-kernel dispatch events in the timed steps, in extra steps after them, or not at all")
     return ap.parse_args()
 
 
-def rank_stream(cfg, world):
-    """The shared stream all ranks draw from, and the per-rank edge count (weak scaling)."""
+def golden_digests():
+    p = os.path.join(ROOT, "tests", "golden", "stream_digests.json")
+    return json.load(open(p)) if os.path.exists(p) else {}
+
+
+def label_digest(labels):
+    """sum_v splitmix64((label[v] << 32) | v) mod 2^64 (the fixture's digest; same formula as the oracle's)."""
+    import numpy as np
+
+    lab = np.asarray(labels, dtype=np.uint64)
+    x = (lab << np.uint64(32)) | np.arange(lab.size, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+        return int(np.sum(x, dtype=np.uint64))
+
+
+def window_starts(cfg, override):
     from gelly_stream import generators as G
 
-    E1, V = cfg.info()
-    if world > 1 and cfg.kind in (2, 3):  # RMAT / GNM: a world-times longer stream over the same ids
-        cfg = G.scaled(cfg, n_edges=cfg.n_edges * world)
-    return cfg, E1, V
+    E, _ = cfg.info()
+    if override:
+        return list(range(0, E, override)) + [E]
+    return [int(x) for x in G.window_starts(cfg)]
+
+
+def rank_chunks(starts, rank, world):
+    """Rank r's contiguous 1/world of every window: [(lo, hi)] per window."""
+    out = []
+    for b, e in zip(starts[:-1], starts[1:]):
+        out.append((b + (e - b) * rank // world, b + (e - b) * (rank + 1) // world))
+    return out
 
 
 def profile_record(workload):
@@ -76,33 +116,207 @@ def profile_record(workload):
     return best
 
 
-def cpu_baseline(cfg, E, V, target_s, threads):
-    """The CPU oracle (restated reference topology) timed on this host: the same stream, one window."""
+def cpu_quota():
+    """CPUs this process may use: cgroup v2 cpu.max quota, else the affinity mask."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(p))))
+    except Exception:
+        pass
+    return n
+
+
+def cpu_baseline(cfg, target_s):
+    """The CPU restatement of the reference (oracle/cc_oracle.c: HashMap union-by-rank DisjointSets, one per
+    partition/thread, serial CombineCC merge into the running summary) timed on this host over a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc  # cpu_baseline leg only
 
     from gelly_stream import generators as G
 
-    pairs = G.generate_host(cfg, 0, E)
-    starts = [0, E]
-    reps, total, digest = 0, 0.0, None
-    while True:
-        out = orc.cc_stream(pairs, starts, V, partitions=threads, threads=threads, want_digest=(reps == 0))
-        if reps == 0:
-            digest = int(out["digest"][0])
-        total += out["fold_seconds"]
-        reps += 1
-        if total >= target_s or reps >= 50:
-            break
+    E, V = cfg.info()
+    n = min(E, CPU_SAMPLE_EDGES)
+    pairs = G.generate_host(cfg, 0, n)
+    nproc = os.cpu_count() or 1
+    res = {}
+    for label, threads in (("t1", 1), ("tquota", cpu_quota()), ("tnproc", nproc)):
+        if label == "tnproc" and threads == res.get("tquota", {}).get("cores"):
+            res[label] = dict(res["tquota"])
+            continue
+        reps, total = 0, 0.0
+        while True:
+            out = orc.cc_stream(pairs, [0, n], V, partitions=threads, threads=threads, want_digest=False)
+            total += out["fold_seconds"]
+            reps += 1
+            if total >= target_s or reps >= 20:
+                break
+        res[label] = {"value": n * reps / total, "cores": threads, "reps": reps, "seconds": round(total, 2)}
+    main = res["tnproc"]
     return {
-        "value": E * reps / total,
-        "unit": "edges/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"full {cfg.name} stream ({E} edges, 1 window) x {reps} reps = {total:.1f} s; "
-                  f"{threads} partitions/threads folding HashMap union-by-rank DisjointSets + serial CombineCC merge "
-                  f"(oracle/cc_oracle.c); host cores visible: {os.cpu_count()}",
-    }, digest
+        "value": main["value"], "unit": "edges/s", "cores": main["cores"], "kind": "port",
+        "sample": f"first {n} edges of the {cfg.name} stream, 1 window; T partitions = T threads folding "
+                  f"HashMap union-by-rank DisjointSets + serial CombineCC merge (oracle/cc_oracle.c); "
+                  f"nproc={nproc}, cpu quota={cpu_quota()}",
+        "t1": res["t1"], "tquota": res["tquota"], "tnproc": res["tnproc"],
+    }
+
+
+def kernel_stats(log, V, inst_steps):
+    """Per-kernel durations from the forest's dispatch-event log, grouped by kernel."""
+    kernel_of = {"filtered": "fold_filtered_kernel", "sample": "fold_kernel", "plain": "fold_kernel",
+                 "seed_hub": "seed_hub_kernel", "seed_bfs": "seed_bfs_kernel", "seed_pack": "seed_pack_kernel",
+                 "seed_init": "seed_pack_kernel", "refresh": "compress_bits_kernel", "compress": "compress_bits_kernel",
+                 "refresh_bits": "compress_bits_kernel", "compress_inc": "compress_inc_kernel",
+                 "refresh_inc": "compress_inc_kernel", "vote": "giant_vote_kernel", "bucket": "bucket_kernel",
+                 "bucket_hist": "bucket_hist_kernel", "slice_filter": "slice_filter_kernel",
+                 "seed_filter": "slice_filter_kernel", "slice_hook": "slice_hook_kernel",
+                 "seed_hook": "slice_hook_kernel", "bucket_init": "bucket_init_kernel", "overflow": "fold_filtered_kernel"}
+    phases, kernels, spans = {}, {}, []
+    for name, ms, n in log:
+        if name in ("begin", "slow_edges"):
+            continue
+        if name == "fold_span":
+            spans.append((ms, n))
+            continue
+        phases.setdefault(name, []).append(ms)
+        kernels.setdefault(kernel_of.get(name, name), []).append((ms, n))
+
+    def kernel_bytes(k, units):
+        per = KERNEL_BYTES.get(k)
+        if per is None:
+            return None
+        return per[0] * (units if per[1] == "edge" else V)
+
+    kstats = {}
+    for k, v in kernels.items():
+        ms_avg = sum(ms for ms, _ in v) / len(v)
+        units = sum(n for _, n in v) / len(v)
+        by = kernel_bytes(k, units)
+        kstats[k] = {"launches_per_step": len(v) / max(1, inst_steps), "ms_avg": ms_avg,
+                     "ms_per_step": sum(ms for ms, _ in v) / max(1, inst_steps), "units_avg": units,
+                     "achieved_gbs": (by / (ms_avg / 1e3) / 1e9) if by and ms_avg > 0 else None}
+    return kstats, phases, spans
+
+
+def make_roofline(kstats, phases, spans, inst_steps, workload, timing_note, host_fold_s):
+    dominant = max(kstats, key=lambda k: kstats[k]["ms_per_step"]) if kstats else None
+    prof = profile_record(workload)
+    dom = kstats.get(dominant, {})
+    achieved = dom.get("achieved_gbs")
+    traffic = None
+    if prof and dominant and dominant in prof.get("kernel", "") and \
+            abs(prof.get("edges_per_launch", 0) - dom.get("units_avg", 0)) <= 0.01 * max(1, dom.get("units_avg", 0)):
+        traffic = prof["hbm_bytes_per_launch"]
+    avg_fold_s = (sum(ms for ms, _ in spans) / len(spans) / 1e3) if spans else None
+    avg_fold_edges = (sum(n for _, n in spans) / len(spans)) if spans else None
+    pipeline_gbs = BYTES_PER_EDGE * avg_fold_edges / avg_fold_s / 1e9 if spans and avg_fold_s else None
+    return {
+        "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+        "traffic": traffic, "traffic_unit": "bytes per launch",
+        "traffic_source": (prof["source"] + (f"; L2 hit rate {prof['l2_hit_rate']:.2f}" if "l2_hit_rate" in prof else ""))
+        if traffic else None,
+        "kernel_ms_avg": dom.get("ms_avg"), "kernel_units_per_launch": int(dom.get("units_avg", 0)),
+        "bytes_per_unit": KERNEL_BYTES.get(dominant), "timing": timing_note, "kernels": kstats,
+        "phases_ms_per_step": {k: sum(v) / max(1, inst_steps) for k, v in phases.items()},
+        "pipeline": {"fold_ms_avg": avg_fold_s * 1e3 if avg_fold_s else None,
+                     "edges_per_fold": int(avg_fold_edges) if avg_fold_edges else None,
+                     "bytes_per_edge": BYTES_PER_EDGE, "achieved": pipeline_gbs,
+                     "frac": (pipeline_gbs / HBM_PEAK_GBS) if pipeline_gbs else None,
+                     "host_enqueue_ms_avg": (sum(host_fold_s) / len(host_fold_s) * 1e3) if host_fold_s else None},
+    }
+
+
+def host_fed_leg(cfg, V, local, steps, tune):
+    """Edges in pinned host memory, folded through gcc_forest_fold_pinned (chunked H2D on a copy stream,
+    overlapped with the folds): the PCIe-inclusive rate (never the headline value)."""
+    import torch
+
+    from gelly_stream import DisjointSet
+    from gelly_stream import generators as G
+
+    E, _ = cfg.info()
+    n = min(E, HOST_FED_MAX_EDGES)
+    d = torch.empty(2 * n, dtype=torch.int32, device=f"cuda:{local}")
+    G.generate_device(cfg, 0, n, d.data_ptr(), torch.cuda.current_stream(local).cuda_stream)
+    h = torch.empty(2 * n, dtype=torch.int32, pin_memory=True)
+    h.copy_(d)
+    torch.cuda.synchronize()
+    del d
+    ds = DisjointSet(V, local)
+    if tune:
+        ds.tune(**tune)
+    ds.reset()
+    ds.fold_pinned(h.data_ptr(), n)
+    ds.sync()
+    reps = max(1, min(steps, 5))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ds.reset()
+        ds.fold_pinned(h.data_ptr(), n)
+        ds.compress()
+        ds.sync()
+    el = (time.perf_counter() - t0) / reps
+    lab = ds.labels()
+    ds.close()
+    return {"value": n / el, "unit": "edges/s", "ms_per_step": el * 1e3, "edges": n,
+            "sample": f"first {n} edges of {cfg.name} in pinned host memory, one window per step",
+            "pcie_gbs": 8 * n / el / 1e9}, lab
+
+
+def c2_rotating_leg(local, steps, warmup, digests, tune):
+    """C2 (R-MAT s20, 16M edges, one window per step) rotating over C2_BATCHES distinct batches."""
+    import torch
+
+    from gelly_stream import DisjointSet
+    from gelly_stream import generators as G
+
+    cfg = G.CONFIGS["c2_rmat20"]
+    E, V = cfg.info()
+    bufs = []
+    for k in range(C2_BATCHES):
+        t = torch.empty(2 * E, dtype=torch.int32, device=f"cuda:{local}")
+        G.generate_device(cfg, k * E, E, t.data_ptr(), torch.cuda.current_stream(local).cuda_stream)
+        bufs.append(t)
+    torch.cuda.synchronize()
+    ds = DisjointSet(V, local)
+    if tune:
+        ds.tune(**tune)
+    ok = True
+
+    def step(i):
+        ds.reset()
+        ds.fold_device(bufs[i % C2_BATCHES].data_ptr(), E)
+        ds.compress()
+
+    for i in range(warmup):
+        step(i)
+    ds.sync()
+    steps = max(steps, 2 * C2_BATCHES)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    ds.sync()
+    el = time.perf_counter() - t0
+    for k in range(C2_BATCHES):  # parity of every batch (after the timed region)
+        step(k)
+        key = "c2_rmat20" if k == 0 else f"c2_rmat20@{k}"
+        if key in digests:
+            ok &= label_digest(ds.labels()) == int(digests[key]["digest"])
+    ds.enable_timing(1)
+    ds.fold_profile()
+    inst = 2 * C2_BATCHES
+    for i in range(inst):
+        step(i)
+    kstats, phases, spans = kernel_stats(ds.fold_profile(), V, inst)
+    ds.enable_timing(0)
+    ds.close()
+    roof = make_roofline(kstats, phases, spans, inst, "c2_rmat20", "dispatch events, after the timed steps", [])
+    return {"value": E * steps / el, "unit": "edges/s", "ms_per_step": el / steps * 1e3, "steps": steps,
+            "batches": C2_BATCHES, "batch_bytes": 8 * E, "parity": "bit-exact" if ok else "MISMATCH",
+            "roofline": {k: roof[k] for k in ("kernel", "achieved", "frac", "kernel_ms_avg", "pipeline")}}
 
 
 def main():
@@ -131,19 +345,25 @@ def main():
     from gelly_stream import generators as G
     from gelly_stream.distributed import ForestGroup, TorchDisjointSet
 
-    base = G.CONFIGS[args.workload]
-    cfg, E1, V = rank_stream(base, world)
-    W = args.window_edges or base.window_edges or E1
-    starts = list(range(0, E1, W)) + [E1]
+    cfg = G.CONFIGS[args.workload]
+    E, V = cfg.info()
+    starts = window_starts(cfg, args.window_edges)
     n_windows = len(starts) - 1
+    chunks = rank_chunks(starts, rank, world)
+    my_edges = sum(hi - lo for lo, hi in chunks)
+    tune = {k: float(v) for k, v in (kv.split("=") for kv in args.tune.split(","))} if args.tune else {}
 
-    # edges of this rank's chunk, generated straight into HBM (outside any timed region)
-    d_edges = torch.empty(2 * E1, dtype=torch.int32, device=f"cuda:{local}")
+    # this rank's chunks of every window, generated straight into HBM (outside any timed region)
+    d_edges = torch.empty(2 * max(1, my_edges), dtype=torch.int32, device=f"cuda:{local}")
     stream = torch.cuda.current_stream(local)
-    G.generate_device(cfg, rank * E1, E1, d_edges.data_ptr(), stream.cuda_stream)
+    offs, off = [], 0
+    for lo, hi in chunks:
+        G.generate_device(cfg, lo, hi - lo, d_edges.data_ptr() + 8 * off, stream.cuda_stream)
+        offs.append((off, hi - lo))
+        off += hi - lo
     forest = TorchDisjointSet(V, local)
-    if args.tune:
-        forest.ds.tune(**{k: float(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
+    if tune:
+        forest.ds.tune(**tune)
     group = ForestGroup() if world > 1 else None
     base_ptr = d_edges.data_ptr()
 
@@ -153,9 +373,9 @@ def main():
     def step(instrument):
         forest.ds.reset()
         for w in range(n_windows):
-            b, e = starts[w], starts[w + 1]
+            o, n = offs[w]
             th = time.perf_counter()
-            forest.ds.fold_device(base_ptr + 8 * b, e - b)
+            forest.ds.fold_device(base_ptr + 8 * o, n)
             if instrument:
                 host_fold_s.append(time.perf_counter() - th)
             if group is not None:
@@ -173,7 +393,7 @@ def main():
     for _ in range(args.warmup):
         step(False)
     # "timed": every kernel of the timed steps carries its own dispatch start/stop events (hipExtLaunchKernel, no
-    # extra packets); "after": the timed steps run bare and min(steps, 10) instrumented steps follow them
+    # extra packets); "after": the timed steps run bare and min(steps, 5) instrumented steps follow them
     timed_inst = args.phase_timing == "timed"
     forest.ds.enable_timing(1 if timed_inst else 0)
     forest.ds.fold_profile()  # drain the warmup log
@@ -195,134 +415,94 @@ def main():
         elapsed = float(t.item())
     inst_steps = args.steps if timed_inst else 0
     if args.phase_timing == "after":
-        inst_steps = min(args.steps, 10)
+        inst_steps = min(args.steps, 5)
         forest.ds.enable_timing(1)
         for _ in range(inst_steps):
             step(True)
         torch.cuda.synchronize()
     log = forest.ds.fold_profile()
     forest.ds.enable_timing(0)
-
-    # per-kernel durations (each kernel's own dispatch events) and per-fold device spans, grouped by kernel
-    kernel_of = {"filtered": "fold_filtered_kernel", "sample": "fold_kernel", "plain": "fold_kernel",
-                 "seed_hub": "seed_hub_kernel", "seed_bfs": "seed_bfs_kernel", "seed_pack": "seed_pack_kernel",
-                 "seed_init": "seed_pack_kernel", "refresh": "compress_bits_kernel", "compress": "compress_bits_kernel", "refresh_bits": "compress_bits_kernel",
-                 "compress_inc": "compress_inc_kernel", "refresh_inc": "compress_inc_kernel",
-                 "vote": "giant_vote_kernel"}
-    phases, kernels, spans = {}, {}, []
-    for name, ms, n in log:
-        if name == "begin" or name == "slow_edges":
-            continue
-        if name == "fold_span":
-            spans.append((ms, n))
-            continue
-        phases.setdefault(name, []).append(ms)
-        kernels.setdefault(kernel_of.get(name, name), []).append((ms, n))
-    avg_fold_s = (sum(ms for ms, _ in spans) / len(spans) / 1e3) if spans else float("nan")
-    avg_fold_edges = (sum(n for _, n in spans) / len(spans)) if spans else E1 / n_windows
-    pipeline_gbs = BYTES_PER_EDGE * avg_fold_edges / avg_fold_s / 1e9 if spans else None
-
-    def kernel_bytes(k, units):
-        """Algorithmic bytes of one launch: per edge for the edge kernels, per id otherwise."""
-        per = KERNEL_BYTES.get(k)
-        if per is None:
-            return None
-        return per[0] * (units if per[1] == "edge" else V)
-
-    kstats = {}
-    for k, v in kernels.items():
-        ms_avg = sum(ms for ms, _ in v) / len(v)
-        units = sum(n for _, n in v) / len(v)
-        by = kernel_bytes(k, units)
-        kstats[k] = {"launches_per_step": len(v) / max(1, inst_steps), "ms_avg": ms_avg,
-                     "ms_per_step": sum(ms for ms, _ in v) / max(1, inst_steps),
-                     "achieved_gbs": (by / (ms_avg / 1e3) / 1e9) if by and ms_avg > 0 else None}
-    prof = profile_record(args.workload)
-    # the dominant kernel: the largest device time per step
-    dominant = max(kstats, key=lambda k: kstats[k]["ms_per_step"]) if kstats else None
-    dom_ms = kstats[dominant]["ms_avg"] if dominant else float("nan")
-    dom_units = (sum(n for _, n in kernels[dominant]) / len(kernels[dominant])) if dominant else 0
-    achieved = kstats[dominant]["achieved_gbs"] if dominant else None
-    traffic = None
-    if prof and dominant and dominant in prof.get("kernel", "") and \
-            abs(prof.get("edges_per_launch", 0) - dom_units) <= 0.01 * max(1, dom_units):
-        traffic = prof["hbm_bytes_per_launch"]
+    kstats, phases, spans = kernel_stats(log, V, inst_steps)
+    timing_note = ("hipExtLaunchKernel dispatch events on the forest's stream, every timed step" if timed_inst
+                   else f"hipExtLaunchKernel dispatch events, {inst_steps} steps after the timed region")
+    roofline = make_roofline(kstats, phases, spans, inst_steps, args.workload, timing_note, host_fold_s)
 
     merge_ms = [a.elapsed_time(b) for a, b in merge_events]
     labels = forest.ds.labels()
     seen = int(np.count_nonzero(labels != 0xFFFFFFFF))
     comps = int(np.count_nonzero(labels == np.arange(V, dtype=np.uint32)))
+    digests = golden_digests()
+    parity = None
+    if not args.no_parity and args.workload in digests:  # any window size: the final partition is the stream's
+        parity = "bit-exact" if label_digest(labels) == int(digests[args.workload]["digest"]) else "MISMATCH"
+    if dist:  # every rank holds the global partition after the merge: all must agree with the fixture
+        ok = torch.tensor([0 if parity == "MISMATCH" else 1], dtype=torch.int32, device=f"cuda:{local}")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if parity is not None and int(ok.item()) == 0:
+            parity = "MISMATCH"
 
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
 
-    total_edges = world * E1 * args.steps
     result = {
         "metric": "edges/sec into CC summary",
-        "value": total_edges / elapsed,
+        "value": E * args.steps / elapsed,
         "unit": "edges/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
         "config": {
-            "workload": f"{base.name}: " + {
+            "workload": f"{cfg.name}: " + {
+                "c1_example": "ConnectedComponentsExample default data, 1000 ms event-time windows",
                 "c2_rmat20": "R-MAT scale 20 (A,B,C,D=0.57,0.19,0.19,0.05), edge factor 16, seeded permutation",
                 "c3_gnm24": "uniform G(n,m) n=2^24 m=9227469",
-                "c4_kron26": "Kronecker scale 26, edge factor 16",
-                "c4_share": "Kronecker scale 26, 2^27 edges per GPU of C4's stream (x8 GPUs = C4's 2^30 edges)",
-                "c5_adversarial": "shuffled 2^23-path + 1024 stars of 8192",
-            }.get(base.name, base.name),
-            "edges_per_gpu": E1,
+                "c4_kron26": "Kronecker scale 26, edge factor 16 (2^30 edges), seeded permutation",
+                "c4_share": "Kronecker scale 26, the first 2^27 edges of C4's stream",
+                "c5_adversarial": "shuffled 2^23-path + 1024 stars of 8192, windows of 2^16 edges",
+            }.get(cfg.name, cfg.name),
+            "stream_edges": E,
+            "edges_per_gpu": my_edges,
             "vertices": V,
             "windows_per_step": n_windows,
-            "window_edges": W,
             "parallelism": f"dp{world}",
+            "partition": "rank r folds the r-th contiguous 1/N of every window (strong scaling of one stream)",
             "merge": ("compact all_gather over RCCL (giant bitmap + others list; label butterfly fallback)"
                       if world > 1 else "none"),
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": dominant,
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": traffic,
-            "traffic_unit": "bytes per launch",
-            "traffic_source": (prof["source"] + f"; L2 hit rate {prof['l2_hit_rate']:.2f}") if traffic else None,
-            "kernel_ms_avg": dom_ms,
-            "kernel_units_per_launch": int(dom_units),
-            "bytes_per_unit": KERNEL_BYTES.get(dominant),
-            "timing": ("hipExtLaunchKernel dispatch events on the forest's stream, every timed step"
-                       if timed_inst else f"hipExtLaunchKernel dispatch events, {inst_steps} steps after the timed region"),
-            "kernels": kstats,
-            "phases_ms_per_step": {k: sum(v) / max(1, inst_steps) for k, v in phases.items()},
-            "pipeline": {"fold_ms_avg": avg_fold_s * 1e3, "edges_per_fold": int(avg_fold_edges),
-                         "bytes_per_edge": BYTES_PER_EDGE, "achieved": pipeline_gbs,
-                         "frac": (pipeline_gbs / HBM_PEAK_GBS) if pipeline_gbs else None,
-                         "host_enqueue_ms_avg": (sum(host_fold_s) / len(host_fold_s) * 1e3) if host_fold_s else None},
-        },
+        "roofline": roofline,
+        "parity": parity,
         "summary": {"seen": seen, "components": comps},
-        "merge": ({"ms_avg": sum(merge_ms) / len(merge_ms), "last": group.last} if group is not None and merge_ms
-                  else None),
+        "merge": ({"ms_avg": sum(merge_ms) / len(merge_ms), "per_window_ms": sum(merge_ms) / len(merge_ms),
+                   "message_bytes": group.last.get("bytes"), "full_label_bytes": 4 * V, "last": group.last}
+                  if group is not None and merge_ms else None),
     }
+    if world == 1 and not args.no_extras:
+        del d_edges
+        forest.ds.close()
+        torch.cuda.empty_cache()
+        try:
+            hf, hl = host_fed_leg(cfg, V, local, args.steps, tune)
+            if hf["edges"] == E and digests.get(args.workload):
+                hf["parity"] = "bit-exact" if label_digest(hl) == int(digests[args.workload]["digest"]) else "MISMATCH"
+            result["host_fed"] = hf
+        except Exception as e:  # a failed extra leg must not hide the headline measurement
+            result["host_fed"] = {"error": repr(e)}
+        torch.cuda.empty_cache()
+        if args.workload != "c2_rmat20":
+            try:
+                result["c2_rotating"] = c2_rotating_leg(local, args.steps, args.warmup, digests, tune)
+            except Exception as e:
+                result["c2_rotating"] = {"error": repr(e)}
     if world == 1 and args.cpu_seconds > 0:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        cb, digest = cpu_baseline(cfg, E1, V, args.cpu_seconds, threads)
-        result["cpu_baseline"] = cb
-        if not args.no_parity:
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            import oracle as orc
-
-            result["parity"] = "bit-exact" if orc.label_digest(labels) == digest else "MISMATCH"
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     print(json.dumps(result))
     if dist:
         dist.destroy_process_group()

@@ -1,0 +1,595 @@
+// bucket_fold.h — the bucketed fold of a FRESH forest over a big id range (DESIGN.md §4 "bucketed fold").
+// Included by gelly_cc.hip after its kernels (uses UF, edge_ok, ring_push / unite_entry, hub_elect).
+//
+// Why: the giant filter of fold_filtered_kernel looks both endpoints of every edge up in a bitmap of the tracked
+// component. At C4 (V = 2^26) that bitmap is 8 MiB — bigger than an XCD's 4 MiB L2 — and the random lookups, not
+// HBM, bound the pass (63 G edges/s for 2 lookups per edge, 824 G edges/s for the same stream with the lookups in
+// LDS; profiles/r2_probe_bucket.log). So the batch is first split by the source id's SLICE (2^19 ids = a 64 KiB
+// slice of the bitmap), and every later pass over an edge finds its bitmap slice in LDS:
+//   bucket_kernel        P1: multi-split of the batch into per-slice buckets (tile-local LDS counting sort, one
+//                        global cursor add per (tile, bucket)); histograms the target ids' slices too
+//   slice_filter_kernel  P2: per bucket, the slice of C in LDS: u in C -> v joins the v-list of v's slice (a 4-B
+//                        multi-split), else (FINAL) the edge takes the union path (per-wave LDS ring)
+//   slice_hook_kernel    P3: per v-list, the slice of C in LDS: v not in C -> SEED: v joins C (LDS bit, OR-ed
+//                        back into the global bitmap); FINAL: v is hooked under g (the edge (u, v) = (g, v))
+// Seeding (C = the component of a hub h, grown over a sample of every bucket by a few P2 + P3 levels), then
+// parent[v] := v in C ? g = min C : UNSEEN (bucket_init_kernel), then P2 + P3 over ALL bucketed edges, then the
+// overflow list (edges a bucket had no room for) and, only if even that list overflowed, the whole batch again
+// (bucket_rest_kernel). Every edge of the batch is folded exactly once by a union or lies inside C, which is one
+// component of the batch: the result is the partition of the batch, whatever the sample or the level count.
+#pragma once
+
+namespace bk {
+
+constexpr u32 kSliceBits = 19;                  // ids per slice: 2^19 -> a 64 KiB bitmap slice in LDS
+constexpr u32 kSliceIds = 1u << kSliceBits;
+constexpr u32 kSliceWords = kSliceIds / 32;     // u32 words per slice (16384)
+constexpr int kP1Block = 512;
+constexpr int kP1Per = 16;                      // edges per thread per tile
+constexpr u32 kP1Tile = kP1Block * kP1Per;      // 8192 edges (64 KiB) per tile
+constexpr int kP2Block = 1024;
+constexpr int kP2Per = 8;                       // edges per thread per round (4 x 16 B)
+constexpr u32 kP2Round = kP2Block * kP2Per;     // 8192 edges per round -> at most 8192 v's per LDS tile
+constexpr u32 kMaxSlicesLds = 512;              // LDS counters: id ranges up to 2^28 (larger: the old path)
+constexpr int kP3Block = 1024;
+constexpr u32 kMaxP2Blocks = 1024;
+
+// Per-forest metadata (device), kMaxSlicesLds entries each where per slice.
+struct Meta {
+    u64 bk_base[kMaxSlicesLds];  // bucket s: edges [bk_base[s], bk_base[s] + bk_cap[s]) of the bucket storage
+    u32 bk_cap[kMaxSlicesLds];
+    u32 bk_cur[kMaxSlicesLds];   // reservation cursor (may pass bk_cap: the rest went to the overflow list)
+    u64 vl_base[kMaxSlicesLds];  // v-list s (targets in slice s): entries [vl_base[s], vl_base[s] + vl_cap[s])
+    u32 vl_cap[kMaxSlicesLds];
+    u32 vl_cur[kMaxSlicesLds];   // may pass vl_cap: those v's were hooked inline (FINAL) or dropped (SEED)
+    u32 work[16];                // per-launch dequeue counters
+    u32 ovf_cur;                 // overflow list cursor (may pass its capacity: then `spill`)
+    u32 spill;                   // 1: some edge fit neither its bucket nor the overflow list
+    u32 gmin;                    // min C (seeding)
+    u32 pad;
+    u32 slow_cnt[kMaxP2Blocks];  // FINAL P2: slow edges (source not in C) each block listed in its own region
+};
+
+__device__ __forceinline__ u32 lds_bit(const u32* s, u32 x) { return (s[x >> 5] >> (x & 31)) & 1u; }
+
+// ---- layout from a strided sample: capacity = 1.25 x the estimated count + slack, for the buckets (by source
+// slice) and the v-lists (by target slice). One block. The sums are bounded by storage_edges() (host) whatever
+// the sample says; a batch the sample misjudges only overflows (overflow list / inline hooks: still exact).
+constexpr u32 kSample = 1u << 16;
+constexpr u32 kSlack = 1u << 12;
+
+__host__ __device__ inline u64 storage_edges(u64 n, u32 ns) { return n + n / 4 + (u64)ns * (kSlack + 64) + 64; }
+
+__device__ __forceinline__ u32 est_cap(u32 hits, u64 n, u64 n_smp) {
+    const u64 est = (u64)hits * n / (n_smp ? n_smp : 1);
+    const u64 c = ((est + est / 4 + kSlack) + 15) / 16 * 16;  // multiples of 16 entries: 16-B aligned runs
+    return (u32)(c < 0xFFFFFFF0ull ? c : 0xFFFFFFF0ull);
+}
+
+// exclusive prefix of cap[0..ns) into base[] (1024 threads, ns <= 1024)
+__device__ __forceinline__ void block_prefix(const u32* cap, u64* base, u32 ns, u64* s_scan) {
+    const u64 loc = threadIdx.x < ns ? cap[threadIdx.x] : 0;
+    s_scan[threadIdx.x] = loc;
+    __syncthreads();
+    for (u32 o = 1; o < 1024; o <<= 1) {  // inclusive scan (Hillis-Steele; 1024 entries, once per batch)
+        const u64 y = threadIdx.x >= o ? s_scan[threadIdx.x - o] : 0;
+        __syncthreads();
+        s_scan[threadIdx.x] += y;
+        __syncthreads();
+    }
+    if (threadIdx.x < ns) base[threadIdx.x] = s_scan[threadIdx.x] - loc;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
+                                                              Meta* __restrict__ m) {
+    __shared__ u32 s_cu[kMaxSlicesLds], s_cv[kMaxSlicesLds];
+    __shared__ u64 s_scan[1024];
+    for (u32 s = threadIdx.x; s < ns; s += 1024) s_cu[s] = s_cv[s] = 0;
+    __syncthreads();
+    const u64 stride = n / kSample ? n / kSample : 1;
+    const u64 n_smp = n < kSample ? n : kSample;
+    for (u64 k = threadIdx.x; k < n_smp; k += 1024) {
+        const u64 e = edges[k * stride];
+        const u32 u = (u32)e, v = (u32)(e >> 32);
+        if (u < cap && v < cap) {
+            atomicAdd(&s_cu[u >> kSliceBits], 1u);
+            atomicAdd(&s_cv[v >> kSliceBits], 1u);
+        }
+    }
+    __syncthreads();
+    for (u32 s = threadIdx.x; s < ns; s += 1024) {
+        m->bk_cap[s] = est_cap(s_cu[s], n, n_smp);
+        m->vl_cap[s] = est_cap(s_cv[s], n, n_smp);
+        m->bk_cur[s] = 0;
+        m->vl_cur[s] = 0;
+    }
+    __syncthreads();
+    block_prefix(m->bk_cap, m->bk_base, ns, s_scan);
+    block_prefix(m->vl_cap, m->vl_base, ns, s_scan);
+    if (threadIdx.x < 16) m->work[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        m->ovf_cur = 0;
+        m->spill = 0;
+    }
+}
+
+// Block-wide exclusive scan of cnt[0..ns) into start[]; returns nothing (BLOCK threads, ns <= kMaxSlicesLds).
+template <int BLOCK>
+__device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u32* s_wsum) {
+    const u32 per = (ns + BLOCK - 1) / BLOCK;
+    u32 loc = 0;
+    for (u32 j = 0; j < per; ++j) {
+        const u32 s = threadIdx.x * per + j;
+        loc += s < ns ? cnt[s] : 0;
+    }
+    const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u32 inc = loc;
+    for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(inc, o, 64);
+        if (lane >= (u32)o) inc += y;
+    }
+    if (lane == 63) s_wsum[wv] = inc;
+    __syncthreads();
+    u32 run = inc - loc;
+    for (u32 w = 0; w < wv; ++w) run += s_wsum[w];
+    for (u32 j = 0; j < per; ++j) {
+        const u32 s = threadIdx.x * per + j;
+        if (s < ns) {
+            start[s] = run;
+            run += cnt[s];
+        }
+    }
+}
+
+// ---- P1: the multi-split -------------------------------------------------------------------------------------
+// Persistent; a tile of kP1Tile edges is counted per bucket in LDS (atomicAdd returns each edge's rank in its
+// bucket), the block reserves each bucket's run with ONE global atomicAdd, scatters the tile into LDS in bucket
+// order and writes every run out contiguously (runs of ~kP1Tile / ns edges). The next tile's loads are in flight
+// meanwhile. Bad ids: skipped + *err. The odd last edge of an odd-length batch and every edge past its bucket's
+// capacity go to the overflow list.
+__global__ __launch_bounds__(kP1Block, 4) void bucket_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
+                                                          Meta* __restrict__ m, u64* __restrict__ bk,
+                                                          u64* __restrict__ ovf, u32 ovf_cap, u32* __restrict__ err) {
+    __shared__ u64 s_srt[kP1Tile];
+    __shared__ u32 s_cnt[kMaxSlicesLds], s_start[kMaxSlicesLds], s_g[kMaxSlicesLds], s_cap[kMaxSlicesLds];
+    __shared__ u64 s_base[kMaxSlicesLds];
+    __shared__ u32 s_wsum[kP1Block / 64];
+    typedef u32 u4 __attribute__((ext_vector_type(4)));
+    const u4* body = reinterpret_cast<const u4*>(edges);  // 16-B aligned (bucket_applies checks)
+    for (u32 s = threadIdx.x; s < ns; s += kP1Block) {  // the layout, once per block (not a global load per edge)
+        s_cap[s] = m->bk_cap[s];
+        s_base[s] = m->bk_base[s];
+    }
+    const u64 n2 = n / 2;                                  // whole pairs
+    const u64 ntiles = (n2 * 2 + kP1Tile - 1) / kP1Tile;
+    constexpr int kQ = kP1Per / 2;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) {  // the odd last edge
+        u32 a = (u32)edges[n - 1], b = (u32)(edges[n - 1] >> 32);
+        if (edge_ok(a, b, cap, err)) {
+            const u32 o = atomicAdd(&m->ovf_cur, 1u);
+            if (o < ovf_cap) ovf[o] = ((u64)b << 32) | a;
+            else m->spill = 1u;
+        }
+    }
+    auto load_tile = [&](u64 t, u4 (&q)[kQ]) {
+#pragma unroll
+        for (int k = 0; k < kQ; ++k) {
+            const u64 j = t * (kP1Tile / 2) + (u64)k * kP1Block + threadIdx.x;
+            q[k] = __builtin_nontemporal_load(body + (j < n2 ? j : n2 - 1));  // clamped: countable loads
+        }
+    };
+    u4 q[kQ];
+    u64 t = blockIdx.x;
+    if (t < ntiles) load_tile(t, q);
+    for (; t < ntiles; t += gridDim.x) {
+        for (u32 s = threadIdx.x; s < ns; s += kP1Block) s_cnt[s] = 0;
+        u32 ua[kP1Per], va[kP1Per], rk[kP1Per];
+        bool ok[kP1Per];
+#pragma unroll
+        for (int k = 0; k < kQ; ++k) {
+            const u64 j = t * (kP1Tile / 2) + (u64)k * kP1Block + threadIdx.x;
+            ua[2 * k] = q[k].x;
+            va[2 * k] = q[k].y;
+            ua[2 * k + 1] = q[k].z;
+            va[2 * k + 1] = q[k].w;
+            ok[2 * k] = ok[2 * k + 1] = j < n2;
+        }
+        if (t + gridDim.x < ntiles) load_tile(t + gridDim.x, q);  // the next tile streams in meanwhile
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kP1Per; ++k) {
+            if (ok[k]) ok[k] = edge_ok(ua[k], va[k], cap, err);
+            if (ok[k]) rk[k] = atomicAdd(&s_cnt[ua[k] >> kSliceBits], 1u);
+        }
+        __syncthreads();
+        count_scan<kP1Block>(s_cnt, s_start, ns, s_wsum);
+        for (u32 s = threadIdx.x; s < ns; s += kP1Block) s_g[s] = s_cnt[s] ? atomicAdd(&m->bk_cur[s], s_cnt[s]) : 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kP1Per; ++k)
+            if (ok[k]) s_srt[s_start[ua[k] >> kSliceBits] + rk[k]] = ((u64)va[k] << 32) | ua[k];
+        __syncthreads();
+        const u32 tot = s_start[ns - 1] + s_cnt[ns - 1];
+        for (u32 x = threadIdx.x; x < tot; x += kP1Block) {
+            const u64 e = s_srt[x];
+            const u32 s = (u32)e >> kSliceBits;
+            const u64 off = (u64)s_g[s] + (x - s_start[s]);
+            if (off < s_cap[s]) {
+                bk[s_base[s] + off] = e;
+            } else {  // the bucket is full (its estimate was low): the overflow list (folded at the end)
+                const u32 o = atomicAdd(&m->ovf_cur, 1u);
+                if (o < ovf_cap) ovf[o] = e;
+                else m->spill = 1u;  // -> bucket_rest_kernel folds the whole batch again (exact, slow)
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Work items of P2 / P3: item i -> (slice i / cps, part i % cps) of a list of `len` entries; the part's range.
+__device__ __forceinline__ void item_range(u64 len, u32 part, u32 cps, u64& lo, u64& hi) {
+    lo = len * part / cps;
+    hi = len * (part + 1) / cps;
+}
+
+// Load slice s of the bitmap (kSliceWords u32) into LDS (16-B loads, 8 in flight per thread).
+template <int BLOCK>
+__device__ __forceinline__ void load_slice(u32* s_bits, const u32* __restrict__ bits, u32 s, u32 nwords32) {
+    typedef u32 u4 __attribute__((ext_vector_type(4)));
+    const u32 w0 = s * kSliceWords;
+    const u32 nw = w0 + kSliceWords <= nwords32 ? kSliceWords : (w0 < nwords32 ? nwords32 - w0 : 0);
+    if (nw == kSliceWords) {
+        lds_fill<BLOCK>(reinterpret_cast<u4*>(s_bits), reinterpret_cast<const u4*>(bits + w0), kSliceWords / 4);
+    } else {  // the last, partial slice
+        for (u32 w = threadIdx.x; w < kSliceWords; w += BLOCK) s_bits[w] = w < nw ? bits[w0 + w] : 0u;
+    }
+}
+
+// The hook of an edge (u, v) with u in C, i.e. union(g, v): unite_entry's hook form — one atomicMin, a union only
+// if v already hung under some other id.
+__device__ __forceinline__ void hook_g(u32* parent, u32 g, u32 v) {
+    NoCount c;
+    if (v > g) {
+        const u32 old = atomicMin(&parent[v], g);
+        if (old != GCC_UNSEEN_DEV && old != v && old != g) UF::unite(parent, g, old, c);
+    } else if (v != g) {
+        UF::unite(parent, g, v, c);
+    }
+}
+
+// ---- P2: filter by the source slice --------------------------------------------------------------------------
+// u in C -> v into the v-lists (SEED: only the first `frac` (16.16 fixed point) of every bucket: the sample).
+// FINAL: an edge whose u is not in C is a SLOW edge: listed in the block's own region of the slow list (no global
+// atomics; past the region's capacity it is united right here through the per-wave LDS ring). A full v-list (its
+// capacity came from a sample): FINAL hooks v under g right here, SEED drops it (seeding is only a heuristic).
+// Rounds of kP2Round edges, the next round's loads in flight; counters double-buffered (3 barriers per round).
+// LDS: slice (64 KiB) + v tile (kP2Round u32) + counters + layout + rings (FINAL).
+template <bool FINAL>
+__global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict__ parent, const u64* __restrict__ bk,
+                                                                const u32* __restrict__ bits, u32 nwords32, u32 ns,
+                                                                Meta* __restrict__ m, u32* __restrict__ vl, u32 cps,
+                                                                u32 frac, u32 work_slot, u32 drain_at,
+                                                                const u32* __restrict__ giant, u64* __restrict__ slow,
+                                                                u32 slow_cap) {
+    extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
+    u32* s_bits = s_dyn;                                   // kSliceWords
+    u32* s_vt = s_dyn + kSliceWords;                       // kP2Round
+    u32* s_cnt2 = s_vt + kP2Round;                         // 2 x kMaxSlicesLds (double-buffered)
+    u32* s_start = s_cnt2 + 2 * kMaxSlicesLds;             // kMaxSlicesLds
+    u32* s_g = s_start + kMaxSlicesLds;                    // kMaxSlicesLds
+    u32* s_vcap = s_g + kMaxSlicesLds;                     // kMaxSlicesLds
+    u64* s_vbase = reinterpret_cast<u64*>(s_vcap + kMaxSlicesLds);      // kMaxSlicesLds
+    u64* ring = s_vbase + kMaxSlicesLds + (threadIdx.x >> 6) * kRing;  // FINAL only
+    __shared__ u32 s_item, s_wsum[kP2Block / 64], s_slow;
+    typedef u32 u4 __attribute__((ext_vector_type(4)));
+    constexpr int kQ = kP2Per / 2;
+    const u32 lane = threadIdx.x & 63;
+    const u32 g = FINAL ? *giant : 0u;
+    u64* my_slow = slow + (u64)blockIdx.x * slow_cap;
+    u32 wq = 0, wd = 0;  // this wave's ring cursors (FINAL)
+    u32 cur_slice = 0xFFFFFFFFu;
+    u32 rb = 0;  // round parity: the counter buffer in use
+    for (u32 s = threadIdx.x; s < 2 * kMaxSlicesLds; s += kP2Block) s_cnt2[s] = 0;
+    for (u32 s = threadIdx.x; s < ns; s += kP2Block) {  // the v-list layout, once per block
+        s_vcap[s] = m->vl_cap[s];
+        s_vbase[s] = m->vl_base[s];
+    }
+    if (threadIdx.x == 0) s_slow = 0;
+    const u32 n_items = ns * cps;
+    while (true) {
+        __syncthreads();
+        if (threadIdx.x == 0) s_item = atomicAdd(&m->work[work_slot], 1u);
+        __syncthreads();
+        const u32 item = s_item;
+        if (item >= n_items) break;
+        const u32 sl = item / cps;
+        u64 len = m->bk_cur[sl] < m->bk_cap[sl] ? m->bk_cur[sl] : m->bk_cap[sl];
+        if (!FINAL) len = len * frac >> 16;
+        u64 lo, hi;
+        item_range(len, item % cps, cps, lo, hi);
+        if (lo >= hi) continue;
+        if (sl != cur_slice) {
+            load_slice<kP2Block>(s_bits, bits, sl, nwords32);
+            cur_slice = sl;
+            __syncthreads();
+        }
+        const u4* eb = reinterpret_cast<const u4*>(bk + m->bk_base[sl]);  // 16-B aligned (16-edge capacities)
+        const u32 sbase = sl << kSliceBits;
+        // pairs [lo / 2, ceil(hi / 2)); edges outside [lo, hi) are masked (a part may start or end mid-pair)
+        const u64 plo = lo / 2, phi = (hi + 1) / 2;
+        u4 q[kQ];
+        auto load_round = [&](u64 p0) {
+#pragma unroll
+            for (int k = 0; k < kQ; ++k) {
+                const u64 j = p0 + (u64)k * kP2Block + threadIdx.x;
+                q[k] = __builtin_nontemporal_load(eb + (j < phi ? j : phi - 1));  // clamped: countable loads
+            }
+        };
+        load_round(plo);
+        for (u64 p0 = plo; p0 < phi; p0 += kP2Round / 2) {
+            u32* s_cnt = s_cnt2 + rb * kMaxSlicesLds;
+            u32 ua[kP2Per], va[kP2Per], rk[kP2Per];
+            bool in[kP2Per];
+#pragma unroll
+            for (int k = 0; k < kQ; ++k) {
+                const u64 j = p0 + (u64)k * kP2Block + threadIdx.x;
+                ua[2 * k] = q[k].x;
+                va[2 * k] = q[k].y;
+                ua[2 * k + 1] = q[k].z;
+                va[2 * k + 1] = q[k].w;
+                in[2 * k] = j < phi && 2 * j >= lo && 2 * j < hi;
+                in[2 * k + 1] = j < phi && 2 * j + 1 >= lo && 2 * j + 1 < hi;
+            }
+            if (p0 + kP2Round / 2 < phi) load_round(p0 + kP2Round / 2);  // next round in flight
+            bool emit[kP2Per];
+#pragma unroll
+            for (int k = 0; k < kP2Per; ++k) {
+                const u32 iu = in[k] ? lds_bit(s_bits, ua[k] - sbase) : 0u;
+                emit[k] = in[k] && iu;
+                if (emit[k]) rk[k] = atomicAdd(&s_cnt[va[k] >> kSliceBits], 1u);
+                if constexpr (FINAL) {  // a slow edge: into this block's region of the slow list (wave-aggregated)
+                    const bool sl_e = in[k] && !iu;
+                    const unsigned long long bm = __ballot(sl_e);
+                    bool spill = false;
+                    if (bm) {
+                        u32 base = 0;
+                        if (lane == 0) base = atomicAdd(&s_slow, (u32)__popcll(bm));
+                        base = __shfl(base, 0, 64);
+                        const u32 pos = base + (u32)__popcll(bm & ((1ull << lane) - 1ull));
+                        if (sl_e) {
+                            if (pos < slow_cap) my_slow[pos] = ((u64)va[k] << 32) | ua[k];
+                            else spill = true;
+                        }
+                    }
+                    ring_push(spill, ua[k], va[k], ring, wq, wd, parent, drain_at, 0xFFFFFFFFu);  // past the region
+                }
+            }
+            __syncthreads();  // (1) counts of this round complete
+            count_scan<kP2Block>(s_cnt, s_start, ns, s_wsum);
+            for (u32 s = threadIdx.x; s < ns; s += kP2Block) {
+                s_g[s] = s_cnt[s] ? atomicAdd(&m->vl_cur[s], s_cnt[s]) : 0;
+                s_cnt2[(rb ^ 1) * kMaxSlicesLds + s] = 0;  // the next round's buffer
+            }
+            __syncthreads();  // (2) starts + reservations
+#pragma unroll
+            for (int k = 0; k < kP2Per; ++k)
+                if (emit[k]) s_vt[s_start[va[k] >> kSliceBits] + rk[k]] = va[k];
+            __syncthreads();  // (3) tile in bucket order
+            const u32 tot = s_start[ns - 1] + s_cnt[ns - 1];
+            for (u32 x = threadIdx.x; x < tot; x += kP2Block) {
+                const u32 v = s_vt[x];
+                const u32 s = v >> kSliceBits;
+                const u64 off = (u64)s_g[s] + (x - s_start[s]);
+                if (off < s_vcap[s]) vl[s_vbase[s] + off] = v;
+                else if (FINAL) hook_g(parent, g, v);  // the v-list is full: (u in C, v) = union(g, v) now
+            }
+            rb ^= 1;  // the write-out above is done before anyone passes the next round's barrier (1)
+        }
+    }
+    if constexpr (FINAL) {  // the rest of this wave's ring; the block's slow count
+        for (; wd < wq; wd += 64) {
+            if (lane < wq - wd) {
+                const u64 e = ring[(wd + lane) & (kRing - 1)];
+                unite_entry(parent, (u32)e, (u32)(e >> 32), 0xFFFFFFFFu);
+            }
+        }
+        if (threadIdx.x == 0) m->slow_cnt[blockIdx.x] = s_slow < slow_cap ? s_slow : slow_cap;
+    }
+}
+
+// ---- P3: the target slice ------------------------------------------------------------------------------------
+// Every v of the slice's v-list that is not in C (LDS slice) is reached from C: it joins the block's LDS copy of
+// the slice (atomicOr). When the block leaves a slice its new members are OR-ed into `out` (one atomicOr per
+// changed word): SEED: out = the bitmap of C itself (C grows for the next level; the block's minimum new id goes
+// to m->gmin); FINAL: out = N, the bitmap of the ids reached from C (bucket_hook_kernel hooks them under g, once
+// each). The v-list streams 16 B per lane, kP3Q loads in flight.
+constexpr int kP3Q = 4;
+template <bool FINAL>
+__global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ bits, u32* __restrict__ out,
+                                                              u32 nwords32, u32 ns, Meta* __restrict__ m,
+                                                              const u32* __restrict__ vl, u32 cps, u32 work_slot) {
+    extern __shared__ __attribute__((aligned(16))) u32 s_bits[];  // kSliceWords
+    __shared__ u32 s_item, s_min;
+    typedef u32 u4 __attribute__((ext_vector_type(4)));
+    u32 cur_slice = 0xFFFFFFFFu;
+    const u32 n_items = ns * cps;
+    u32 lmin = 0xFFFFFFFFu;
+    auto flush_slice = [&]() {  // this block's new members of cur_slice -> out
+        if (cur_slice == 0xFFFFFFFFu) return;
+        const u32 w0 = cur_slice * kSliceWords;
+        for (u32 w = threadIdx.x; w < kSliceWords && w0 + w < nwords32; w += kP3Block) {
+            const u32 nw = s_bits[w] & ~bits[w0 + w];
+            if (nw && (!FINAL || (nw & ~out[w0 + w]))) atomicOr(&out[w0 + w], nw);
+        }
+    };
+    auto visit = [&](u32 v, u32 sbase) {
+        const u32 x = v - sbase, msk = 1u << (x & 31);
+        if (s_bits[x >> 5] & msk) return;                  // already in C (or taken by this block)
+        if (atomicOr(&s_bits[x >> 5], msk) & msk) return;  // another lane of the block took it
+        if (!FINAL) lmin = v < lmin ? v : lmin;
+    };
+    while (true) {
+        __syncthreads();
+        if (threadIdx.x == 0) s_item = atomicAdd(&m->work[work_slot], 1u);
+        __syncthreads();
+        const u32 item = s_item;
+        if (item >= n_items) break;
+        const u32 sl = item / cps;
+        const u64 len = m->vl_cur[sl] < m->vl_cap[sl] ? m->vl_cur[sl] : m->vl_cap[sl];
+        u64 lo, hi;
+        item_range(len, item % cps, cps, lo, hi);
+        if (lo >= hi) continue;
+        if (sl != cur_slice) {
+            flush_slice();
+            __syncthreads();
+            load_slice<kP3Block>(s_bits, bits, sl, nwords32);
+            cur_slice = sl;
+            __syncthreads();
+        }
+        const u32* v0 = vl + m->vl_base[sl];  // 16-B aligned
+        const u32 sbase = sl << kSliceBits;
+        const u64 qlo = lo / 4, qhi = (hi + 3) / 4;  // 4-entry groups; entries outside [lo, hi) masked
+        for (u64 b = qlo; b < qhi; b += (u64)kP3Q * kP3Block) {
+            u4 r[kP3Q];
+#pragma unroll
+            for (int k = 0; k < kP3Q; ++k) {
+                const u64 j = b + (u64)k * kP3Block + threadIdx.x;
+                r[k] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(v0) + (j < qhi ? j : qhi - 1));
+            }
+#pragma unroll
+            for (int k = 0; k < kP3Q; ++k) {
+                const u64 j = b + (u64)k * kP3Block + threadIdx.x;
+                if (j >= qhi) continue;
+                const u64 e = 4 * j;
+                if (e >= lo && e < hi) visit(r[k].x, sbase);
+                if (e + 1 >= lo && e + 1 < hi) visit(r[k].y, sbase);
+                if (e + 2 >= lo && e + 2 < hi) visit(r[k].z, sbase);
+                if (e + 3 >= lo && e + 3 < hi) visit(r[k].w, sbase);
+            }
+        }
+    }
+    __syncthreads();
+    flush_slice();
+    if constexpr (!FINAL) {
+        for (int o = 32; o > 0; o >>= 1) lmin = min(lmin, (u32)__shfl_down(lmin, o, 64));
+        if (threadIdx.x == 0) s_min = 0xFFFFFFFFu;
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0 && lmin != 0xFFFFFFFFu) atomicMin(&s_min, lmin);
+        __syncthreads();
+        if (threadIdx.x == 0 && s_min != 0xFFFFFFFFu) atomicMin(&m->gmin, s_min);
+    }
+}
+
+// N (ids reached from C by the FINAL pass) joins g's tree, each id once: a new id above g by a plain store (in this
+// kernel nothing else writes an UNSEEN slot: the hooks below only touch seen ids and roots), anything else by
+// hook_g. The tracked component's bitmap becomes C | N (one component: g's), N is cleared for the next batch.
+__global__ __launch_bounds__(kBlock) void bucket_hook_kernel(u32* __restrict__ parent, u32* __restrict__ bits,
+                                                             u32* __restrict__ nbits, u32 nwords32,
+                                                             const u32* __restrict__ giant) {
+    const u32 g = *giant;
+    for (u64 w = (u64)blockIdx.x * kBlock + threadIdx.x; w < nwords32; w += (u64)gridDim.x * kBlock) {
+        u32 d = nbits[w];
+        if (!d) continue;
+        nbits[w] = 0;
+        d &= ~bits[w];
+        if (!d || g == GCC_UNSEEN_DEV) continue;
+        bits[w] |= d;
+        while (d) {
+            const u32 k = (u32)__builtin_ctz(d);
+            d &= d - 1;
+            const u32 v = (u32)(w * 32 + k);
+            if (v > g && parent[v] == GCC_UNSEEN_DEV) parent[v] = g;
+            else hook_g(parent, g, v);
+        }
+    }
+}
+
+// The slow list (FINAL P2: edges whose source was not in C) against C | N: both ends in it -> already connected to
+// g; one end -> the other hooked under g; neither -> united.
+__global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ parent, const u64* __restrict__ slow,
+                                                             u32 slow_cap, const Meta* __restrict__ m, u32 nblocks,
+                                                             const u32* __restrict__ bits, const u32* __restrict__ giant) {
+    const u32 g = *giant;
+    NoCount c;
+    const u64 total = (u64)nblocks * slow_cap;
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < total; i += (u64)gridDim.x * kBlock) {
+        const u32 r = (u32)(i / slow_cap), k = (u32)(i - (u64)r * slow_cap);
+        if (k >= m->slow_cnt[r]) continue;
+        const u64 e = slow[i];
+        const u32 a = (u32)e, b = (u32)(e >> 32);
+        const u32 ia = lds_bit(bits, a), ib = lds_bit(bits, b);
+        if (ia & ib) continue;
+        if (ia) hook_g(parent, g, b);
+        else if (ib) hook_g(parent, g, a);
+        else UF::unite(parent, a, b, c);
+    }
+}
+
+// Seeding start: clear the bitmap (done by the host's memset), elect the hub h of the batch's first edges (the
+// same deterministic election as the seeded fold), C := {h}, gmin := h. One block.
+__global__ __launch_bounds__(kHubBlock) void bucket_hub_kernel(const u64* __restrict__ edges, u64 n, u32 cap,
+                                                               u32* __restrict__ bits, Meta* __restrict__ m) {
+    extern __shared__ __attribute__((aligned(16))) u32 s_tab[];
+    u64 e[kHubPer];
+    hub_sample(edges, n < kHubSample ? n : kHubSample, e);
+    const u32 h = hub_elect(e, s_tab, cap);
+    if (threadIdx.x == 0) {
+        m->gmin = h;
+        if (h != GCC_UNSEEN_DEV) bits[h >> 5] = 1u << (h & 31);
+    }
+}
+
+// parent[v] := v in C ? g : UNSEEN over the whole id range (the reset and all of C's unions in one write);
+// giant := g. 4 ids per lane, 16-B stores.
+__global__ __launch_bounds__(kBlock) void bucket_init_kernel(u32* __restrict__ parent, u32 n,
+                                                             const u32* __restrict__ bits, const Meta* __restrict__ m,
+                                                             u32* __restrict__ giant) {
+    const u32 g = m->gmin;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *giant = g;
+    typedef u32 u4 __attribute__((ext_vector_type(4)));
+    const u64 nq = ((u64)n + 3) / 4;
+    for (u64 q = (u64)blockIdx.x * kBlock + threadIdx.x; q < nq; q += (u64)gridDim.x * kBlock) {
+        const u32 w = bits[q >> 3] >> ((q & 7) * 4);
+        const u64 v = 4 * q;
+        if (v + 3 < n) {
+            u4 o;
+            o.x = (w & 1u) ? g : GCC_UNSEEN_DEV;
+            o.y = (w & 2u) ? g : GCC_UNSEEN_DEV;
+            o.z = (w & 4u) ? g : GCC_UNSEEN_DEV;
+            o.w = (w & 8u) ? g : GCC_UNSEEN_DEV;
+            reinterpret_cast<u4*>(parent)[q] = o;
+        } else {
+            for (u32 k = 0; k < 4; ++k)
+                if (v + k < n) parent[v + k] = ((w >> k) & 1u) ? g : GCC_UNSEEN_DEV;
+        }
+    }
+}
+
+// The overflow list (edges their bucket had no room for): united, skipped when both ends are in C. If the list
+// itself overflowed (spill), the WHOLE batch is united again: exact (union is idempotent), only slow.
+__global__ __launch_bounds__(kBlock) void bucket_rest_kernel(u32* __restrict__ parent, const u64* __restrict__ ovf,
+                                                             u32 ovf_cap, const Meta* __restrict__ m,
+                                                             const u32* __restrict__ bits,
+                                                             const u64* __restrict__ edges, u64 n, u32 cap,
+                                                             u32* __restrict__ err) {
+    NoCount c;
+    const u64 stride = (u64)gridDim.x * kBlock;
+    const u64 no = m->ovf_cur < ovf_cap ? m->ovf_cur : ovf_cap;
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < no; i += stride) {
+        const u64 e = ovf[i];
+        const u32 a = (u32)e, b = (u32)(e >> 32);
+        if (lds_bit(bits, a) & lds_bit(bits, b)) continue;
+        UF::unite(parent, a, b, c);
+    }
+    if (m->spill) {
+        for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+            const u64 e = edges[i];
+            u32 a = (u32)e, b = (u32)(e >> 32);
+            if (!edge_ok(a, b, cap, err)) continue;
+            UF::unite(parent, a, b, c);
+        }
+    }
+}
+
+}  // namespace bk

@@ -29,6 +29,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -77,15 +78,31 @@ constexpr unsigned kMaxGrid = 2048;         // 256 CUs x 8 resident 256-thread b
 // coalesced non-temporal stream (read once; it must not evict parent[] lines from L2).
 // REC: every id that leaves UNSEEN or root state is marked in bloom (uf_device.h BloomRec), so the next
 // compress can be incremental (compress_inc_kernel).
+// Device-side id validation (gcc_forest_fold_device takes raw device pairs): an edge with an id >= cap is
+// skipped — never dereferenced — and *err is set; the host reports it at the next synchronising call
+// (stream_sync_checked). The ids of a bad edge are replaced by 0 so that later bitmap lookups stay in range.
+__device__ __forceinline__ bool edge_ok(u32& a, u32& b, u32 cap, u32* err) {
+    const bool ok = a < cap && b < cap;
+    if (!ok) {
+        *err = 1u;
+        a = 0;
+        b = 0;
+    }
+    return ok;
+}
+
 template <bool REC>
 __global__ __launch_bounds__(kBlock) void fold_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
-                                                      u64 n_edges, u32* __restrict__ bloom) {
+                                                      u64 n_edges, u32* __restrict__ bloom, u32 cap,
+                                                      u32* __restrict__ err) {
     NoCount c;
     const u64 stride = (u64)gridDim.x * kBlock;
     for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n_edges; i += stride) {
         const u64 e = __builtin_nontemporal_load(edges + i);
-        if constexpr (REC) UF::unite(parent, (u32)e, (u32)(e >> 32), c, gcc::BloomRec{bloom});
-        else UF::unite(parent, (u32)e, (u32)(e >> 32), c);
+        u32 a = (u32)e, b = (u32)(e >> 32);
+        if (!edge_ok(a, b, cap, err)) continue;
+        if constexpr (REC) UF::unite(parent, a, b, c, gcc::BloomRec{bloom});
+        else UF::unite(parent, a, b, c);
     }
 }
 
@@ -233,7 +250,8 @@ template <bool LDS, int BLOCK, int DEPTH, bool PIPE, bool HOOK>
 __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
                                                               u64 n_edges, const u32* __restrict__ bits, u32 nwords,
                                                               const u32* __restrict__ giant,
-                                                              u32* __restrict__ slow_count, u32 drain_at) {
+                                                              u32* __restrict__ slow_count, u32 drain_at, u32 cap,
+                                                              u32* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     __shared__ u32 s_slow;
     const u32 bitmap_u32 = LDS ? nwords * 2 : 0;  // nwords = u64 words, even
@@ -289,18 +307,21 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
                     u32 ea[2 * DEPTH], eb[2 * DEPTH];
 #pragma unroll
                     for (int k = 0; k < DEPTH; ++k) {
-                        vv[2 * k] = vv[2 * k + 1] = true;
                         ea[2 * k] = q[k].x;
                         eb[2 * k] = q[k].y;
                         ea[2 * k + 1] = q[k].z;
                         eb[2 * k + 1] = q[k].w;
+                        vv[2 * k] = edge_ok(ea[2 * k], eb[2 * k], cap, err);
+                        vv[2 * k + 1] = edge_ok(ea[2 * k + 1], eb[2 * k + 1], cap, err);
                     }
                     filter_round<LDS, 2 * DEPTH>(vv, ea, eb, bm, g, ring, wq, wd, parent, drain_at, carry);
                 } else {
 #pragma unroll
                     for (int k = 0; k < DEPTH; ++k) {
-                        filter_edge<LDS>(true, q[k].x, q[k].y, bm, g, ring, wq, wd, parent, drain_at);
-                        filter_edge<LDS>(true, q[k].z, q[k].w, bm, g, ring, wq, wd, parent, drain_at);
+                        u32 a0 = q[k].x, b0 = q[k].y, a1 = q[k].z, b1 = q[k].w;
+                        const bool v0 = edge_ok(a0, b0, cap, err), v1 = edge_ok(a1, b1, cap, err);
+                        filter_edge<LDS>(v0, a0, b0, bm, g, ring, wq, wd, parent, drain_at);
+                        filter_edge<LDS>(v1, a1, b1, bm, g, ring, wq, wd, parent, drain_at);
                     }
                 }
                 base = nb;
@@ -317,8 +338,10 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
             for (int k = 0; k < DEPTH; ++k) q[k] = __builtin_nontemporal_load(body + i + k * stride);
 #pragma unroll
             for (int k = 0; k < DEPTH; ++k) {
-                filter_edge<LDS>(true, q[k].x, q[k].y, bm, g, ring, wq, wd, parent, drain_at);
-                filter_edge<LDS>(true, q[k].z, q[k].w, bm, g, ring, wq, wd, parent, drain_at);
+                u32 a0 = q[k].x, b0 = q[k].y, a1 = q[k].z, b1 = q[k].w;
+                const bool v0 = edge_ok(a0, b0, cap, err), v1 = edge_ok(a1, b1, cap, err);
+                filter_edge<LDS>(v0, a0, b0, bm, g, ring, wq, wd, parent, drain_at);
+                filter_edge<LDS>(v1, a1, b1, bm, g, ring, wq, wd, parent, drain_at);
             }
         }
     }
@@ -327,13 +350,14 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
         const bool valid = i < n2;
         u32x4 q = {0, 0, 0, 0};
         if (valid) q = __builtin_nontemporal_load(body + i);
+        u32 ea[2] = {q.x, q.z}, eb[2] = {q.y, q.w};
+        const bool v0 = edge_ok(ea[0], eb[0], cap, err) && valid, v1 = edge_ok(ea[1], eb[1], cap, err) && valid;
         if constexpr (HOOK) {
-            const bool vv[2] = {valid, valid};
-            const u32 ea[2] = {q.x, q.z}, eb[2] = {q.y, q.w};
+            const bool vv[2] = {v0, v1};
             filter_round<LDS, 2>(vv, ea, eb, bm, g, ring, wq, wd, parent, drain_at, carry2);
         } else {
-            filter_edge<LDS>(valid, q.x, q.y, bm, g, ring, wq, wd, parent, drain_at);
-            filter_edge<LDS>(valid, q.z, q.w, bm, g, ring, wq, wd, parent, drain_at);
+            filter_edge<LDS>(v0, ea[0], eb[0], bm, g, ring, wq, wd, parent, drain_at);
+            filter_edge<LDS>(v1, ea[1], eb[1], bm, g, ring, wq, wd, parent, drain_at);
         }
     }
     if constexpr (HOOK) {  // the last rounds' hooks
@@ -350,10 +374,14 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
     }
     if (lane == 0 && wq) atomicAdd(&s_slow, wq);
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // scalar head / tail edges
-        if (head) UF::unite(parent, (u32)edges[0], (u32)(edges[0] >> 32), c);
+        if (head) {
+            u32 a = (u32)edges[0], b = (u32)(edges[0] >> 32);
+            if (edge_ok(a, b, cap, err)) UF::unite(parent, a, b, c);
+        }
         if (head + 2 * n2 < n_edges) {
             const u64 e = edges[n_edges - 1];
-            UF::unite(parent, (u32)e, (u32)(e >> 32), c);
+            u32 a = (u32)e, b = (u32)(e >> 32);
+            if (edge_ok(a, b, cap, err)) UF::unite(parent, a, b, c);
         }
     }
     __syncthreads();
@@ -640,7 +668,7 @@ __device__ __forceinline__ void hub_sample(const u64* __restrict__ edges, u64 n_
     }
 }
 
-__device__ __forceinline__ u32 hub_elect(const u64 (&e)[kHubPer], u32* s_tab) {
+__device__ __forceinline__ u32 hub_elect(const u64 (&e)[kHubPer], u32* s_tab, u32 cap) {
     u32* s_key = s_tab;
     u32* s_cnt = s_tab + kHubSlots;
     __shared__ u32 s_bc[kHubBlock / 64], s_bk[kHubBlock / 64];
@@ -660,6 +688,7 @@ __device__ __forceinline__ u32 hub_elect(const u64 (&e)[kHubPer], u32* s_tab) {
     for (int k = 0; k < kPer; ++k) {
         if (e[k] == ~0ull) continue;
         const u32 a = (u32)e[k], b = (u32)(e[k] >> 32);
+        if (a >= cap || b >= cap) continue;  // a bad edge is flagged by the pass that folds it
         const u32 ca = hub_count(a, s_key, s_cnt);
         if (hub_better(ca, a, bc, bk)) {
             bc = ca;
@@ -695,7 +724,8 @@ __device__ __forceinline__ u32 hub_elect(const u64 (&e)[kHubPer], u32* s_tab) {
             bk = k2;
         }
     }
-    return __shfl(bk, 0, 64);  // n_sample >= 1, so some endpoint was counted
+    // UNSEEN when no sampled edge was valid: the seeding then starts from C = {} (every edge takes the union path)
+    return __shfl(bk, 0, 64);
 }
 
 // Elects h and initialises C = {h}: flags (zeroed up to a whole bitmap word) and the bitmap. Every block of
@@ -706,7 +736,7 @@ __global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restri
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     u64 e[kHubPer];
     hub_sample(edges, n_sample, e);
-    const u32 h = hub_elect(e, s_dyn);
+    const u32 h = hub_elect(e, s_dyn, n);
     // this block's share: 32 ids per unit = 32 flag bytes (two 16-B stores) + one bitmap word
     const u64 nu = ((u64)n + 31) / 32;
     const u64 per = (nu + gridDim.x - 1) / gridDim.x;
@@ -737,7 +767,8 @@ __global__ __launch_bounds__(kHubBlock) void seed_hub_kernel(const u64* __restri
 template <bool LDS, int BLOCK, bool NT, bool HUB>
 __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__ edges, u64 n,
                                                          const u32* __restrict__ bits32, u32 nwords32,
-                                                         u8* __restrict__ flags, u32* __restrict__ bmin, u8 epoch) {
+                                                         u8* __restrict__ flags, u32* __restrict__ bmin, u8 epoch,
+                                                         u32 cap, u32* __restrict__ err) {
     static_assert(!HUB || (LDS && BLOCK == kHubBlock), "the fused hub election needs the LDS variant");
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     __shared__ u32 s_min;
@@ -767,11 +798,11 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
     if (threadIdx.x == 0) s_min = UNSEEN;
     u32 lmin = UNSEEN;
     if constexpr (HUB) {
-        const u32 h = hub_elect(e, s_dyn);  // ends with a barrier
+        const u32 h = hub_elect(e, s_dyn, cap);  // ends with a barrier
         const u32x4 z = {0, 0, 0, 0};
         for (u32 w = threadIdx.x; w < nwords32 / 4; w += BLOCK) reinterpret_cast<u32x4*>(s_dyn)[w] = z;
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == 0 && h != UNSEEN) {
             s_dyn[h >> 5] = 1u << (h & 31);
             if (blockIdx.x == 0) {
                 flags[h] = epoch;
@@ -787,6 +818,7 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
     }
     __syncthreads();
     auto visit = [&](u32 a, u32 b) {
+        if (!edge_ok(a, b, cap, err)) return;
         const u32 ia = (bm[a >> 5] >> (a & 31)) & 1u, ib = (bm[b >> 5] >> (b & 31)) & 1u;
         if (ia != ib) {
             const u32 x = ia ? b : a, m = 1u << (x & 31);
@@ -1080,6 +1112,13 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
     }
 }
 
+#include "bucket_fold.h"
+
+static constexpr size_t slice_filter_lds() {  // bucket_fold.h slice_filter_kernel's dynamic LDS
+    return (bk::kSliceWords + bk::kP2Round + 5 * bk::kMaxSlicesLds) * sizeof(u32) + bk::kMaxSlicesLds * sizeof(u64) +
+           (bk::kP2Block / 64) * kRing * sizeof(u64);
+}
+
 // counts[0] += #seen, counts[1] += #roots (= #components)
 __global__ __launch_bounds__(kBlock) void count_kernel(const u32* __restrict__ parent, u32 n,
                                                        unsigned long long* __restrict__ counts) {
@@ -1163,6 +1202,15 @@ struct FoldTune {
     bool inc_inplace = true;  // the incremental compress rewrites only changed parent[] slots (no spare buffer)
     u64 inc_min_ids = 1ull << 22;
     u64 inc_div = 8;
+    // bucketed fold of a fresh forest (bucket_fold.h): batches of >= bucket_min_batch edges over >= bucket_min_ids
+    // ids (default: exactly the forests whose giant bitmap does not fit LDS); seeding = bucket_levels P2 + P3 levels
+    // over the first bucket_sample of every bucket
+    bool bucket = true;
+    u64 bucket_min_batch = 1ull << 25;
+    u64 bucket_min_ids = (u64)kLdsBitmapMaxWords * 64 + 1;
+    int bucket_levels = 3;
+    double bucket_sample = 0.25;
+    u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -1215,6 +1263,30 @@ struct gcc_forest {
     bool witness_armed = false;  // the last encode already reset d_witness (stream-ordered before the next absorb)
 
     unsigned long long* d_counts = nullptr;
+
+    // device-side id validation of raw device batches (edge_ok): set by a kernel, reported and cleared by the next
+    // synchronising call (stream_sync_checked)
+    u32* d_err = nullptr;
+    u32* h_err = nullptr;  // pinned copy
+
+    // gcc_forest_fold_pinned: chunks of a pinned host batch go H2D on copy_stream into two device slots while
+    // the previous chunk folds on `stream`
+    hipStream_t copy_stream = nullptr;
+    u32* d_pin[2] = {nullptr, nullptr};
+    u64 pin_cap = 0;  // edges per slot
+    hipEvent_t pin_copied[2] = {nullptr, nullptr}, pin_folded[2] = {nullptr, nullptr};
+
+    // bucketed fold (bucket_fold.h): metadata, bucket storage, overflow list, v-lists (grown on demand)
+    bk::Meta* d_meta = nullptr;
+    u64* d_bk = nullptr;
+    u64 bk_cap_edges = 0;
+    u64* d_ovf = nullptr;
+    u64 ovf_cap = 0;
+    u32* d_vl = nullptr;
+    u64 vl_cap = 0;
+    u64* d_slow = nullptr;  // FINAL P2's slow edges, one region per block
+    u64 slow_cap_total = 0;
+    u32* d_nbits = nullptr;  // N: ids reached from C by the FINAL pass (kept all-zero between batches)
 
     // lazy host view of the labels (getMatches()/find() consumers)
     std::vector<u32> host_labels;
@@ -1290,6 +1362,20 @@ static int launch_k(gcc_forest* h, const char* name, u64 edges, F kernel, dim3 g
     return GCC_OK;
 }
 
+// Synchronise the handle's stream and report an id-range error that a kernel recorded since the last check
+// (edge_ok: those edges were skipped, the batch's other edges folded). Every synchronising entry point uses it.
+static int stream_sync_checked(gcc_forest* h) {
+    HIP_TRY(hipMemcpyAsync(h->h_err, h->d_err, sizeof(u32), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (*h->h_err) {
+        *h->h_err = 0;
+        HIP_TRY(hipMemsetAsync(h->d_err, 0, sizeof(u32), h->stream));
+        return set_err(GCC_E_INVALID, "a device batch held a vertex id >= id_capacity %u (those edges were skipped)",
+                       h->cap);
+    }
+    return GCC_OK;
+}
+
 static int materialize_reset(gcc_forest* h) {
     if (!h->pending_reset) return GCC_OK;
     h->rec_all = false;
@@ -1334,12 +1420,6 @@ static int compress_now(gcc_forest* h, const char* name = "compress") {
                           h->d_giant + h->giant_slot, h->d_giant + 4);
         u32* clear = h->d_bloom ? h->bloom(h->bloom_cur ^ 1) : nullptr;
         if (!rc && inc_here && h->rec_all) {
-            static bool attr = false;
-            if (!attr) {
-                for (const void* f : {(const void*)compress_inc_kernel<false>, (const void*)compress_inc_kernel<true>})
-                    HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(gcc::kBloomBits / 8)));
-                attr = true;
-            }
             const char* kname = std::strcmp(name, "refresh") ? "compress_inc" : "refresh_inc";
             inplace = h->tune.inc_inplace;
             rc = inplace ? launch_k(h, kname, 0, compress_inc_kernel<true>, dim3(h->n_cu), dim3(kIncBlock),
@@ -1391,10 +1471,10 @@ static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* na
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
     if (h->rec_all && n * std::max<u64>(1, h->tune.inc_div) <= (u64)h->cap)
         return launch_k(h, name, n, fold_kernel<true>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent, edges,
-                        n, h->bloom(h->bloom_cur));
+                        n, h->bloom(h->bloom_cur), h->cap, h->d_err);
     h->rec_all = false;
     return launch_k(h, name, n, fold_kernel<false>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent, edges, n,
-                    (u32*)nullptr);
+                    (u32*)nullptr, h->cap, h->d_err);
 }
 
 static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
@@ -1413,19 +1493,10 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
     int rc = GCC_OK;
     if (lds) {
         const size_t lds_bytes = (size_t)nw * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64);
-        static bool lds_attr_set = false;  // > 64 KiB of dynamic LDS must be allowed explicitly (once per process)
-        if (!lds_attr_set) {
-            const int max_lds = (int)(kLdsBitmapMaxWords * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64));
-            const void* fns[4] = {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, false>,
-                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true, false>,
-                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, true>,
-                                  (const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true, true>};
-            for (const void* f : fns) HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds));
-            lds_attr_set = true;
-        }
 #define GCC_FILTERED(D, H)                                                                                     \
     launch_k(h, "filtered", n, fold_filtered_kernel<true, kFilterBlockLds, D, true, H>, dim3(nblocks),         \
-             dim3(kFilterBlockLds), lds_bytes, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
+             dim3(kFilterBlockLds), lds_bytes, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at,   \
+             h->cap, h->d_err)
         switch (variant) {
         case 0: rc = GCC_FILTERED(4, false); break;
         case 1: rc = GCC_FILTERED(8, false); break;
@@ -1437,7 +1508,7 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
         const size_t lds_bytes = (kBlock / 64) * kRing * sizeof(u64);
 #define GCC_FILTERED(D, H)                                                                                  \
     launch_k(h, "filtered", n, fold_filtered_kernel<false, kBlock, D, true, H>, dim3(nblocks), dim3(kBlock), \
-             lds_bytes, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at)
+             lds_bytes, h->d_parent, edges, n, bits, nw, giant, h->d_qcount, h->tune.drain_at, h->cap, h->d_err)
         switch (variant) {
         case 0: rc = GCC_FILTERED(4, false); break;
         case 1: rc = GCC_FILTERED(8, false); break;
@@ -1492,12 +1563,6 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
     } else {
         flags = reinterpret_cast<u8*>(h->d_spare);  // free until the next compress: one flag byte per id
         const unsigned hub_grid = (unsigned)std::max<u64>(1, std::min<u64>((u64)h->n_cu, (u64)h->cap >> 16));
-        static bool hub_attr = false;
-        if (!hub_attr) {
-            HIP_TRY(hipFuncSetAttribute((const void*)seed_hub_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)(2 * kHubSlots * sizeof(u32))));
-            hub_attr = true;
-        }
         rc = launch_k(h, "seed_hub", 0, seed_hub_kernel, dim3(hub_grid), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32),
                       edges, std::min(n, kHubSample), flags, bits, h->cap, gmin);
         if (rc) return rc;
@@ -1510,31 +1575,23 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
     for (int p = 0; p < t.seed_passes; ++p) {
         const u64 np = p == 0 ? pref1 : pref;
         if (lds) {
-            static bool attr = false;
-            if (!attr) {
-                for (const void* f : {(const void*)seed_bfs_kernel<true, kFilterBlockLds, true, false>,
-                                      (const void*)seed_bfs_kernel<true, kFilterBlockLds, false, false>,
-                                      (const void*)seed_bfs_kernel<true, kFilterBlockLds, true, true>,
-                                      (const void*)seed_bfs_kernel<true, kFilterBlockLds, false, true>})
-                    HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                (int)(kLdsBitmapMaxWords * sizeof(u64))));
-                attr = true;
-            }
             const bool hub = fuse && p == 0;
             // the fused first pass also holds the election's hash table (2 x kHubSlots u32) in the same LDS
             const size_t sh = std::max<size_t>((size_t)nw32 * sizeof(u32), hub ? 2 * kHubSlots * sizeof(u32) : 0);
 #define GCC_BFS(NT, HUB)                                                                                       \
     launch_k(h, "seed_bfs", np, seed_bfs_kernel<true, kFilterBlockLds, NT, HUB>, dim3(h->n_cu), dim3(kFilterBlockLds), \
-             sh, edges, np, (const u32*)bits, nw32, flags, h->d_bmin + n_bmin, epoch)
+             sh, edges, np, (const u32*)bits, nw32, flags, h->d_bmin + n_bmin, epoch, h->cap, h->d_err)
             rc = t.seed_nt ? (hub ? GCC_BFS(true, true) : GCC_BFS(true, false))
                            : (hub ? GCC_BFS(false, true) : GCC_BFS(false, false));
 #undef GCC_BFS
         } else {
             const unsigned grid = grid_for((np + 1) / 2, kMaxGrid);
             rc = t.seed_nt ? launch_k(h, "seed_bfs", np, seed_bfs_kernel<false, kBlock, true, false>, dim3(grid),
-                                      dim3(kBlock), 0, edges, np, (const u32*)bits, nw32, flags, h->d_bmin + n_bmin, epoch)
+                                      dim3(kBlock), 0, edges, np, (const u32*)bits, nw32, flags, h->d_bmin + n_bmin, epoch,
+                                      h->cap, h->d_err)
                            : launch_k(h, "seed_bfs", np, seed_bfs_kernel<false, kBlock, false, false>, dim3(grid),
-                                      dim3(kBlock), 0, edges, np, (const u32*)bits, nw32, flags, h->d_bmin + n_bmin, epoch);
+                                      dim3(kBlock), 0, edges, np, (const u32*)bits, nw32, flags, h->d_bmin + n_bmin, epoch,
+                                      h->cap, h->d_err);
             n_bmin += grid;
         }
         if (rc) return rc;
@@ -1549,6 +1606,106 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
     rc = launch_k(h, "seed_init", 0, seed_pack_kernel<true>, dim3(pack_grid), dim3(kBlock), 0, h->d_parent, h->cap,
                   (const u8*)flags, bits, (const u32*)(fuse ? h->d_bmin + 1 : h->d_bmin), fuse ? n_bmin - 1 : n_bmin,
                   h->d_giant + h->giant_slot, epoch);
+    if (rc) return rc;
+    h->pending_reset = false;
+    h->has_giant = true;
+    return GCC_OK;
+}
+
+// The bucketed fold of a fresh forest (bucket_fold.h): when it applies, and the pipeline.
+static u32 bucket_slices(const gcc_forest* h) { return (u32)(((u64)h->cap + bk::kSliceIds - 1) / bk::kSliceIds); }
+
+static bool bucket_applies(const gcc_forest* h, const u32* d_pairs, u64 n) {
+    const FoldTune& t = h->tune;
+    return t.bucket && h->pending_reset && h->filter_enabled() && (u64)h->cap >= t.bucket_min_ids &&
+           n >= std::max<u64>(t.bucket_min_batch, 2 * bk::kP1Tile) && n < (1ull << 31) &&
+           bucket_slices(h) <= bk::kMaxSlicesLds &&
+           ((reinterpret_cast<uintptr_t>(d_pairs) | reinterpret_cast<uintptr_t>(h->d_parent) |
+             reinterpret_cast<uintptr_t>(h->d_spare)) & 15) == 0;
+}
+
+template <typename T>
+static int grow(T*& p, u64& cap, u64 need) {
+    if (cap >= need) return GCC_OK;
+    if (p) HIP_TRY(hipFree(p));
+    p = nullptr;
+    cap = 0;
+    HIP_TRY(hipMalloc((void**)&p, (size_t)need * sizeof(T)));
+    cap = need;
+    return GCC_OK;
+}
+
+static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
+    const FoldTune& t = h->tune;
+    h->rec_all = false;
+    int rc = alloc_filter(h);
+    if (rc) return rc;
+    const u32 ns = bucket_slices(h);
+    if (!h->d_meta) HIP_TRY(hipMalloc((void**)&h->d_meta, sizeof(bk::Meta)));
+    if ((rc = grow(h->d_bk, h->bk_cap_edges, bk::storage_edges(n, ns)))) return rc;
+    if ((rc = grow(h->d_ovf, h->ovf_cap, n / 8 + 65536))) return rc;
+    if ((rc = grow(h->d_vl, h->vl_cap, bk::storage_edges(n, ns)))) return rc;
+    const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
+    const u32 slow_cap = (u32)std::min<u64>(0x7FFFFFFFull, std::max<u64>(4096, n / p2_blocks / 8));
+    if ((rc = grow(h->d_slow, h->slow_cap_total, (u64)p2_blocks * slow_cap))) return rc;
+    const u64* edges = reinterpret_cast<const u64*>(d_pairs);
+    u32* bits = reinterpret_cast<u32*>(h->d_bits);
+    const u32 nw32 = 2 * (h->nwords() + (h->nwords() & 1));
+    u32* giant = h->d_giant + h->giant_slot;
+    if (!h->d_nbits) {
+        HIP_TRY(hipMalloc((void**)&h->d_nbits, (size_t)nw32 * sizeof(u32)));
+        HIP_TRY(hipMemsetAsync(h->d_nbits, 0, (size_t)nw32 * sizeof(u32), h->stream));
+    }
+    const u32 ovf_cap = (u32)std::min<u64>(h->ovf_cap, 0xFFFFFFF0ull);
+    const u32 items = 4 * (u32)h->n_cu;  // dequeue items per P2 / P3 launch (parts of the slices)
+    const u32 cps = std::max<u32>(1, (items + ns - 1) / ns);
+    const size_t f_lds = slice_filter_lds(), h_lds = bk::kSliceWords * sizeof(u32);
+    const size_t vl_cur_off = offsetof(bk::Meta, vl_cur);
+    u32 slot = 0;
+    rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta);
+    if (!rc)
+        rc = launch_k(h, "bucket", n, bk::bucket_kernel, dim3(2 * h->n_cu), dim3(bk::kP1Block), 0, edges, n, ns, h->cap,
+                      h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err);
+    if (rc) return rc;
+    // seeding: C := {hub}, then levels over the sample
+    HIP_TRY(hipMemsetAsync(bits, 0, (size_t)nw32 * sizeof(u32), h->stream));
+    rc = launch_k(h, "bucket_hub", 0, bk::bucket_hub_kernel, dim3(1), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32), edges,
+                  n, h->cap, bits, h->d_meta);
+    const u32 frac = (u32)std::max(0.0, std::min(65536.0, t.bucket_sample * 65536.0));
+    const u64 sample_edges = (u64)((double)n * frac / 65536.0);
+    const int levels = std::max(0, std::min(6, t.bucket_levels));
+    for (int l = 0; l < levels && !rc; ++l) {
+        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
+        rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
+                      f_lds, h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps, frac,
+                      slot++, h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap);
+        if (!rc)
+            rc = launch_k(h, "seed_hook", 0, bk::slice_hook_kernel<false>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
+                          bits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++);
+    }
+    // parent[] := C ? g : UNSEEN (the reset), then every bucketed edge, the overflow list, a spill
+    if (!rc)
+        rc = launch_k(h, "bucket_init", 0, bk::bucket_init_kernel, dim3(grid_for(((u64)h->cap + 3) / 4, kMaxGrid)),
+                      dim3(kBlock), 0, h->d_parent, h->cap, (const u32*)bits, (const bk::Meta*)h->d_meta, giant);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
+    rc = launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true>, dim3(p2_blocks), dim3(bk::kP2Block), f_lds,
+                  h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps, 65536u, slot++,
+                  h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap);
+    if (!rc)
+        rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
+                      h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++);
+    if (!rc)
+        rc = launch_k(h, "bucket_hook", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
+                      h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
+    if (!rc)
+        rc = launch_k(h, "bucket_slow", 0, bk::bucket_slow_kernel, dim3(grid_for((u64)p2_blocks * slow_cap, kMaxGrid)),
+                      dim3(kBlock), 0, h->d_parent, (const u64*)h->d_slow, slow_cap, (const bk::Meta*)h->d_meta, p2_blocks,
+                      (const u32*)bits, (const u32*)giant);
+    if (!rc)
+        rc = launch_k(h, "bucket_rest", 0, bk::bucket_rest_kernel, dim3(grid_for(n / 64 + 1, kMaxGrid)), dim3(kBlock), 0,
+                      h->d_parent, (const u64*)h->d_ovf, ovf_cap, (const bk::Meta*)h->d_meta, (const u32*)bits, edges, n,
+                      h->cap, h->d_err);
     if (rc) return rc;
     h->pending_reset = false;
     h->has_giant = true;
@@ -1577,6 +1734,16 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
                         n >= 64 &&
                         ((reinterpret_cast<uintptr_t>(h->d_parent) | reinterpret_cast<uintptr_t>(h->d_spare)) & 15) == 0;
     double refresh[3] = {t.refresh[0], t.refresh[1], t.refresh[2]};
+    if (bucket_applies(h, d_pairs, n)) {  // a fresh forest over a big id range: the bucketed fold
+        rc = launch_bucket(h, d_pairs, n);
+        if (rc) return rc;
+        if (h->timing && (int)h->kev_used > ev_first) {
+            h->last_fold_first = ev_first;
+            h->last_fold_last = (int)h->kev_used - 1;
+        }
+        mark_mutated(h);
+        return GCC_OK;
+    }
     if (seeded) {
         rc = launch_seed(h, d_pairs, n);
         refresh[0] = t.seed_refresh;
@@ -1691,7 +1858,8 @@ static int refresh_host(gcc_forest* h) {
     h->host_labels.resize(h->cap);
     HIP_TRY(hipMemcpyAsync(h->host_labels.data(), h->d_parent, (size_t)h->cap * sizeof(u32), hipMemcpyDeviceToHost,
                            h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    rc = stream_sync_checked(h);
+    if (rc) return rc;
     h->host_valid = true;
     return GCC_OK;
 }
@@ -1705,8 +1873,7 @@ static int counts(gcc_forest* h, unsigned long long out[2]) {
                        h->d_counts);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out, h->d_counts, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    return GCC_OK;
+    return stream_sync_checked(h);
 }
 // ------------------------------------------------------------------------------------------------
 // C ABI
@@ -1767,6 +1934,52 @@ int gcc_gen_device(const gcc_gen_params* p, uint64_t first, uint64_t count, uint
     return GCC_OK;
 }
 
+// Kernels with > 64 KiB of dynamic LDS must be allowed it explicitly, and the attribute belongs to the function's
+// code object on ONE device: it is set once per device (std::call_once per device index: thread-safe for task
+// threads creating forests on several GPUs at once), before the device's first forest exists.
+constexpr int kMaxDevices = 64;
+static std::once_flag g_attr_once[kMaxDevices];
+static int g_attr_rc[kMaxDevices];
+static std::string g_attr_msg[kMaxDevices];
+
+static int set_lds_attrs_impl() {
+    const int filtered = (int)(kLdsBitmapMaxWords * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64));
+    const int bitmap = (int)(kLdsBitmapMaxWords * sizeof(u64));
+    const struct {
+        const void* f;
+        int bytes;
+    } tab[] = {
+        {(const void*)compress_inc_kernel<false>, (int)(gcc::kBloomBits / 8)},
+        {(const void*)compress_inc_kernel<true>, (int)(gcc::kBloomBits / 8)},
+        {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, false>, filtered},
+        {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true, false>, filtered},
+        {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, true>, filtered},
+        {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true, true>, filtered},
+        {(const void*)seed_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
+        {(const void*)seed_bfs_kernel<true, kFilterBlockLds, true, false>, bitmap},
+        {(const void*)seed_bfs_kernel<true, kFilterBlockLds, false, false>, bitmap},
+        {(const void*)seed_bfs_kernel<true, kFilterBlockLds, true, true>, bitmap},
+        {(const void*)seed_bfs_kernel<true, kFilterBlockLds, false, true>, bitmap},
+        {(const void*)bk::slice_filter_kernel<false>, (int)slice_filter_lds()},
+        {(const void*)bk::slice_filter_kernel<true>, (int)slice_filter_lds()},
+        {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kSliceWords * sizeof(u32))},
+        {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kSliceWords * sizeof(u32))},
+        {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
+    };
+    for (const auto& t : tab) HIP_TRY(hipFuncSetAttribute(t.f, hipFuncAttributeMaxDynamicSharedMemorySize, t.bytes));
+    return GCC_OK;
+}
+
+static int ensure_lds_attrs(int device) {  // `device` is current
+    if (device < 0 || device >= kMaxDevices) return set_err(GCC_E_INVALID, "device %d beyond %d", device, kMaxDevices);
+    std::call_once(g_attr_once[device], [device] {
+        g_attr_rc[device] = set_lds_attrs_impl();
+        if (g_attr_rc[device]) g_attr_msg[device] = g_last_error;
+    });
+    if (g_attr_rc[device]) return set_err(g_attr_rc[device], "%s", g_attr_msg[device].c_str());
+    return GCC_OK;
+}
+
 static int forest_create_impl(int device, uint32_t id_capacity, uint32_t* d_buf0, uint32_t* d_buf1,
                               gcc_forest** out) {
     CHECK_ARG(out, "out is null");
@@ -1775,6 +1988,8 @@ static int forest_create_impl(int device, uint32_t id_capacity, uint32_t* d_buf0
     int rc = gcc_check_device(device);
     if (rc) return rc;
     DeviceGuard g(device);
+    rc = ensure_lds_attrs(device);
+    if (rc) return rc;
     gcc_forest* h = new gcc_forest();
     h->device = device;
     h->cap = id_capacity;
@@ -1790,6 +2005,11 @@ static int forest_create_impl(int device, uint32_t id_capacity, uint32_t* d_buf0
     hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) return fail(set_err(GCC_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e)));
     h->stream = h->own_stream;
+    e = hipMalloc((void**)&h->d_err, sizeof(u32));
+    if (e == hipSuccess) e = hipMemset(h->d_err, 0, sizeof(u32));
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_err, sizeof(u32), hipHostMallocDefault);
+    if (e != hipSuccess) return fail(set_err(GCC_E_HIP, "error word: %s", hipGetErrorString(e)));
+    *h->h_err = 0;
     if (d_buf0) {
         h->d_parent = d_buf0;
         h->d_spare = d_buf1;
@@ -1836,6 +2056,23 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (h->d_bmin) (void)hipFree(h->d_bmin);
     if (h->d_qcount) (void)hipFree(h->d_qcount);
     if (h->d_counts) (void)hipFree(h->d_counts);
+    if (h->d_err) (void)hipFree(h->d_err);
+    if (h->d_meta) (void)hipFree(h->d_meta);
+    if (h->d_bk) (void)hipFree(h->d_bk);
+    if (h->d_ovf) (void)hipFree(h->d_ovf);
+    if (h->d_vl) (void)hipFree(h->d_vl);
+    if (h->d_slow) (void)hipFree(h->d_slow);
+    if (h->d_nbits) (void)hipFree(h->d_nbits);
+    if (h->h_err) (void)hipHostFree(h->h_err);
+    for (int s = 0; s < 2; ++s) {
+        if (h->d_pin[s]) (void)hipFree(h->d_pin[s]);
+        if (h->pin_copied[s]) (void)hipEventDestroy(h->pin_copied[s]);
+        if (h->pin_folded[s]) (void)hipEventDestroy(h->pin_folded[s]);
+    }
+    if (h->copy_stream) {
+        (void)hipStreamSynchronize(h->copy_stream);
+        (void)hipStreamDestroy(h->copy_stream);
+    }
     for (auto& pe : h->kev) {
         (void)hipEventDestroy(pe.first);
         (void)hipEventDestroy(pe.second);
@@ -1881,8 +2118,19 @@ int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent) {
     DeviceGuard g(h->device);
     int rc = flush(h);
     if (rc) return rc;
-    h->rec_all = false;  // the caller may write through the pointer: no incremental compress until a full one
+    // the caller may write through the pointer: nothing cached about parent[] holds any more (no incremental
+    // compress until a full one; the next read compresses and re-reads)
+    mark_mutated(h);
     *d_parent = h->d_parent;
+    return GCC_OK;
+}
+
+int gcc_forest_labels_device(gcc_forest* h, const uint32_t** d_labels) {
+    CHECK_ARG(h && d_labels, "null argument");
+    DeviceGuard g(h->device);
+    int rc = compress_async(h);  // read-only view: the forest's caches (rec_all, compressed) stay valid
+    if (rc) return rc;
+    *d_labels = h->d_parent;
     return GCC_OK;
 }
 
@@ -1977,6 +2225,54 @@ int gcc_forest_fold_device(gcc_forest* h, const uint32_t* d_pairs, uint64_t n_ed
     return launch_fold(h, d_pairs, n_edges);
 }
 
+// Pinned host batch (the JNI / FFM direct-buffer path): chunks (tune.pin_chunk edges) go H2D on the handle's copy
+// stream into two device slots while the previous chunk folds on the handle's stream; ids are validated on the
+// device (edge_ok). Each chunk is one batch of the fold pipeline. Asynchronous: `pairs` must stay valid until the
+// next synchronising call.
+
+int gcc_forest_fold_pinned(gcc_forest* h, const uint32_t* pairs, uint64_t n_edges) {
+    CHECK_ARG(h, "null forest");
+    CHECK_ARG(pairs || n_edges == 0, "pairs is null");
+    DeviceGuard g(h->device);
+    int rc = flush_staged(h);
+    if (rc) return rc;
+    if (n_edges == 0) return GCC_OK;
+    const u64 chunk = std::min<u64>(n_edges, std::max<u64>(1024, h->tune.pin_chunk));
+    if (!h->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+    if (!h->pin_copied[0]) {
+        for (int s = 0; s < 2; ++s) {
+            HIP_TRY(hipEventCreateWithFlags(&h->pin_copied[s], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&h->pin_folded[s], hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(h->pin_folded[s], h->stream));
+        }
+    }
+    if (h->pin_cap < chunk) {  // grow the slots (both streams idle first: a slot may still be read)
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        HIP_TRY(hipStreamSynchronize(h->copy_stream));
+        for (int s = 0; s < 2; ++s) {
+            if (h->d_pin[s]) HIP_TRY(hipFree(h->d_pin[s]));
+            h->d_pin[s] = nullptr;
+        }
+        h->pin_cap = 0;
+        for (int s = 0; s < 2; ++s) HIP_TRY(hipMalloc((void**)&h->d_pin[s], (size_t)chunk * 2 * sizeof(u32)));
+        h->pin_cap = chunk;
+    }
+    for (u64 b = 0, k = 0; b < n_edges; b += chunk, ++k) {
+        const int s = (int)(k & 1);
+        const u64 m = std::min<u64>(chunk, n_edges - b);
+        HIP_TRY(hipStreamWaitEvent(h->copy_stream, h->pin_folded[s], 0));  // the slot's last fold is done
+        HIP_TRY(hipMemcpyAsync(h->d_pin[s], pairs + 2 * b, (size_t)m * 2 * sizeof(u32), hipMemcpyHostToDevice,
+                               h->copy_stream));
+        HIP_TRY(hipEventRecord(h->pin_copied[s], h->copy_stream));
+        HIP_TRY(hipStreamWaitEvent(h->stream, h->pin_copied[s], 0));
+        rc = launch_fold(h, h->d_pin[s], m);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(h->pin_folded[s], h->stream));
+    }
+    h->host_valid = false;
+    return GCC_OK;
+}
+
 int gcc_forest_flush(gcc_forest* h) {
     CHECK_ARG(h, "null forest");
     DeviceGuard g(h->device);
@@ -1988,8 +2284,7 @@ int gcc_forest_sync(gcc_forest* h) {
     DeviceGuard g(h->device);
     int rc = flush(h);
     if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    return GCC_OK;
+    return stream_sync_checked(h);
 }
 
 int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, uint32_t n) {
@@ -2021,30 +2316,45 @@ int gcc_forest_merge(gcc_forest* into, gcc_forest* from) {
     DeviceGuard g(into->device);
     int rc = flush(into);
     if (rc) return rc;
-    // order into's stream after everything queued on from's stream
-    hipEvent_t ev;
+    // Two events, each created on the device whose stream records it: ev_from orders into's stream after everything
+    // queued on from's stream; ev_into orders from's stream after the merge has read from's parent[] (from must
+    // not be mutated before). Both are destroyed on every path.
+    hipEvent_t ev_from = nullptr, ev_into = nullptr;
+    auto done = [&](int code) {
+        if (ev_from) {
+            DeviceGuard gf(from->device);
+            (void)hipEventDestroy(ev_from);
+        }
+        if (ev_into) (void)hipEventDestroy(ev_into);
+        return code;
+    };
+    auto hip = [&](hipError_t e, const char* what) {
+        return e == hipSuccess ? GCC_OK : set_err(GCC_E_HIP, "gcc_forest_merge: %s: %s", what, hipGetErrorString(e));
+    };
     {
         DeviceGuard gf(from->device);
-        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(ev, from->stream));
+        rc = hip(hipEventCreateWithFlags(&ev_from, hipEventDisableTiming), "event (from)");
+        if (!rc) rc = hip(hipEventRecord(ev_from, from->stream), "record (from)");
     }
-    HIP_TRY(hipStreamWaitEvent(into->stream, ev, 0));
+    if (!rc) rc = hip(hipEventCreateWithFlags(&ev_into, hipEventDisableTiming), "event (into)");
+    if (!rc) rc = hip(hipStreamWaitEvent(into->stream, ev_from, 0), "wait (into)");
+    if (rc) return done(rc);
     const u32* src = from->d_parent;
     if (from->device != into->device) {
-        if (!into->d_scratch) HIP_TRY(hipMalloc((void**)&into->d_scratch, (size_t)into->cap * sizeof(u32)));
-        HIP_TRY(hipMemcpyPeerAsync(into->d_scratch, into->device, from->d_parent, from->device,
-                                   (size_t)from->cap * sizeof(u32), into->stream));
+        if (!into->d_scratch) rc = hip(hipMalloc((void**)&into->d_scratch, (size_t)into->cap * sizeof(u32)), "scratch");
+        if (!rc)
+            rc = hip(hipMemcpyPeerAsync(into->d_scratch, into->device, from->d_parent, from->device,
+                                        (size_t)from->cap * sizeof(u32), into->stream), "peer copy");
         src = into->d_scratch;
     }
-    rc = gcc_forest_merge_labels_device(into, src, from->cap);
-    // from must not be mutated before the merge has read it
-    HIP_TRY(hipEventRecord(ev, into->stream));
-    {
+    if (!rc) rc = gcc_forest_merge_labels_device(into, src, from->cap);
+    // whatever was enqueued on into's stream, from waits for it before its next mutation
+    int rc2 = hip(hipEventRecord(ev_into, into->stream), "record (into)");
+    if (!rc2) {
         DeviceGuard gf(from->device);
-        HIP_TRY(hipStreamWaitEvent(from->stream, ev, 0));
+        rc2 = hip(hipStreamWaitEvent(from->stream, ev_into, 0), "wait (from)");
     }
-    HIP_TRY(hipEventDestroy(ev));
-    return rc;
+    return done(rc ? rc : rc2);
 }
 
 uint64_t gcc_msg_bytes(uint32_t id_capacity, uint64_t cap_others) {
@@ -2136,8 +2446,7 @@ int gcc_forest_raw_parent(gcc_forest* h, uint32_t* out, uint32_t n) {
     int rc = flush(h);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(out, h->d_parent, (size_t)n * sizeof(u32), hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    return GCC_OK;
+    return stream_sync_checked(h);
 }
 
 int gcc_forest_find(gcc_forest* h, uint32_t v, uint32_t* root) {
@@ -2214,6 +2523,12 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "refresh_labels") t.refresh_labels = value != 0;
     else if (k == "inc_min_ids") t.inc_min_ids = (u64)value;
     else if (k == "inc_div") t.inc_div = std::max<u64>(1, (u64)value);
+    else if (k == "pin_chunk") t.pin_chunk = (u64)value;
+    else if (k == "bucket") t.bucket = value != 0;
+    else if (k == "bucket_min_batch") t.bucket_min_batch = (u64)value;
+    else if (k == "bucket_min_ids") t.bucket_min_ids = (u64)value;
+    else if (k == "bucket_levels") t.bucket_levels = std::max(0, std::min(6, (int)value));
+    else if (k == "bucket_sample") t.bucket_sample = std::max(0.0, std::min(1.0, value));
     else return set_err(GCC_E_INVALID, "unknown tuning key '%s'", key);
     return GCC_OK;
 }

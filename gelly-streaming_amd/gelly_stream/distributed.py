@@ -54,8 +54,8 @@ class TorchDisjointSet:
         self.ds.compress()
 
     def exchange_tensor(self):
-        """The tensor that currently holds the forest (the canonical labels right after compress())."""
-        cur = self.ds.device_ptr()
+        """The tensor holding the canonical labels (read-only view: the forest's incremental-compress state stays)."""
+        cur = self.ds.labels_device()
         return self.bufs[0] if self.bufs[0].data_ptr() == cur else self.bufs[1]
 
     def absorb(self, labels) -> None:

@@ -144,16 +144,19 @@ class LongDisjointSet:
         if ids.size:
             self.fold(np.stack([ids, lab], axis=1))
 
-    def _labels(self) -> np.ndarray:
+    def _labels(self) -> tuple[np.ndarray, np.ndarray]:
+        """(canonical label per dense id, seen mask per dense id). Seen-ness comes from the forest (dense label !=
+        UNSEEN), never from a sentinel value: every Long, Long.MAX_VALUE included, is a valid label."""
         if self._cache is None:
-            self._cache = self.dict.canonical(self.forest.labels())
+            dense = self.forest.labels()
+            lab = self.dict.canonical(dense)
+            self._cache = (lab, dense[:lab.size] != UNSEEN)
         return self._cache
 
     def seen_labels(self) -> tuple[np.ndarray, np.ndarray]:
         """(original ids seen, their canonical labels)."""
-        lab = self._labels()
+        lab, seen = self._labels()
         ids = self.dict.ids()
-        seen = lab != _I64_MAX
         return ids[seen], lab[seen]
 
     def find(self, e: int) -> Optional[int]:
@@ -161,8 +164,8 @@ class LongDisjointSet:
         d = self.dict.lookup(e)
         if d is None:
             return None
-        r = int(self._labels()[d])
-        return None if r == _I64_MAX else r
+        lab, seen = self._labels()
+        return int(lab[d]) if seen[d] else None
 
     def getMatches(self) -> LongMatchesView:
         return LongMatchesView(self)

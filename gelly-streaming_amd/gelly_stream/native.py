@@ -71,6 +71,8 @@ _SIGS = {
     "gcc_forest_submit": (c_int, [c_void_p, c_uint64]),
     "gcc_forest_fold_host": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_forest_fold_device": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_forest_fold_pinned": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_forest_labels_device": (c_int, [c_void_p, POINTER(c_void_p)]),
     "gcc_forest_flush": (c_int, [c_void_p]),
     "gcc_forest_sync": (c_int, [c_void_p]),
     "gcc_forest_merge": (c_int, [c_void_p, c_void_p]),

@@ -173,6 +173,19 @@ class DisjointSet:
         call("gcc_forest_fold_device", self.handle, c_void_p(d_pairs), int(n_edges))
         self._dirty()
 
+    def fold_pinned(self, h_pairs: int, n_edges: int) -> None:
+        """Fold n_edges interleaved u32 pairs in pinned host memory (chunked H2D overlapped with the folds; async:
+        the buffer must stay valid until the next synchronising call, e.g. sync())."""
+        call("gcc_forest_fold_pinned", self.handle, c_void_p(h_pairs), int(n_edges))
+        self._dirty()
+
+    def labels_device(self) -> int:
+        """Compress (async) and return the device buffer of the canonical labels, read-only (valid until the next
+        mutation of this forest)."""
+        p = c_void_p()
+        call("gcc_forest_labels_device", self.handle, byref(p))
+        return p.value
+
     def merge_labels_device(self, d_labels: int, n: int) -> None:
         """self := self ∪ {(v, labels[v])} for a device label/parent array (the cross-GPU merge receive)."""
         call("gcc_forest_merge_labels_device", self.handle, c_void_p(d_labels), int(n))

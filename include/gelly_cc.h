@@ -91,7 +91,12 @@ int gcc_forest_destroy(gcc_forest* h);
 int gcc_forest_set_stream(gcc_forest* h, void* hip_stream, int use_own);
 int gcc_forest_get_stream(gcc_forest* h, void** hip_stream);
 int gcc_forest_capacity(gcc_forest* h, uint32_t* id_capacity);
-int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent); /* current forest (= labels after compress) */
+/* current forest buffer (= labels after compress); the caller may WRITE through it, so every cached view of the
+ * forest is dropped (the next read compresses again) */
+int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent);
+/* compress (async) and return the canonical labels' device buffer, READ-ONLY (valid until the handle's next
+ * mutation): the send side of a cross-GPU label exchange */
+int gcc_forest_labels_device(gcc_forest* h, const uint32_t** d_labels);
 /* back to the initial value (SummaryAggregation.Merger transientState reset, :113-115; fresh fold value) */
 int gcc_forest_reset(gcc_forest* h);
 
@@ -101,7 +106,14 @@ int gcc_forest_make_set(gcc_forest* h, uint32_t v);          /* DisjointSet.make
 int gcc_forest_staging(gcc_forest* h, uint32_t** pairs, uint64_t* cap_edges); /* pinned host staging buffer */
 int gcc_forest_submit(gcc_forest* h, uint64_t n_edges);      /* fold the first n_edges of staging (async) */
 int gcc_forest_fold_host(gcc_forest* h, const uint32_t* pairs, uint64_t n_edges); /* pageable host pairs */
-int gcc_forest_fold_device(gcc_forest* h, const uint32_t* d_pairs, uint64_t n_edges); /* pairs in HBM, async */
+/* pairs in HBM, async. Ids are validated on the device: an edge with an id >= id_capacity is skipped (never
+ * dereferenced) and the next synchronising call on the handle (labels / find / size / sync / ...) returns
+ * GCC_E_INVALID once for it; the batch's other edges are folded. */
+int gcc_forest_fold_device(gcc_forest* h, const uint32_t* d_pairs, uint64_t n_edges);
+/* pairs in PINNED host memory (hipHostMalloc / hipHostRegister / a JNI direct ByteBuffer's registered pages), async:
+ * chunked H2D on the handle's copy stream overlapped with the folds, ids validated on the device as above. The
+ * buffer must stay valid and unmodified until the next synchronising call (e.g. gcc_forest_sync). */
+int gcc_forest_fold_pinned(gcc_forest* h, const uint32_t* pairs, uint64_t n_edges);
 int gcc_forest_flush(gcc_forest* h); /* launch any staged single-edge unions */
 int gcc_forest_sync(gcc_forest* h);  /* flush + wait for the handle's stream */
 
@@ -187,7 +199,8 @@ int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, 
 /* fold-pipeline tuning knobs; results never depend on them, only speed does. Keys: filter, filter_min_batch,
  * filter_min_share, sample_first, sample_growth, sample_div, sample_min, refresh_min_batch, refresh1..refresh3, depth, hook,
  * drain_at, seed, seed_nt, seed_global, seed_fuse, seed_passes, seed_div, seed_div1, seed_refresh, incremental,
- * inc_min_ids, inc_div, inc_inplace, refresh_labels. Unknown keys return GCC_E_INVALID. */
+ * inc_min_ids, inc_div, inc_inplace, refresh_labels, bucket, bucket_min_batch, bucket_min_ids, bucket_levels,
+ * bucket_sample, pin_chunk. Unknown keys return GCC_E_INVALID. */
 int gcc_forest_tune(gcc_forest* h, const char* key, double value);
 
 #ifdef __cplusplus

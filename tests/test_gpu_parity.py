@@ -521,6 +521,13 @@ KNOB_CASES = {
     "inc_min_ids": {"inc_min_ids": 1024}, "inc_div": {"inc_min_ids": 1024, "inc_div": 1},
     "inc_inplace": {"inc_min_ids": 1024, "inc_inplace": 0},
     "refresh_labels": {"refresh_min_batch": 1024, "refresh_labels": 1},
+    # the bucketed fold (bucket_fold.h) at this size only when forced by bucket_min_ids / bucket_min_batch
+    "bucket": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket": 0},
+    "bucket_min_batch": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16},
+    "bucket_min_ids": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16},
+    "bucket_levels": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_levels": 1},
+    "bucket_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_sample": 1.0},
+    "pin_chunk": {"pin_chunk": 4096},
 }
 
 

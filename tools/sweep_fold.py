@@ -38,10 +38,10 @@ def main():
     G.generate_device(cfg, 0, E, d.data_ptr(), 0)
     torch.cuda.synchronize()
     t = time.time()
-    cache = os.path.join(ROOT, "tools", "digests.json")
+    cache = os.path.join(ROOT, "tests", "golden", "stream_digests.json")
     known = json.load(open(cache)).get(wl) if os.path.exists(cache) else None
-    if known:  # oracle digest computed on the CPU by tools/make_digests.py
-        want = known["digest"]
+    if known:  # oracle digest computed on the CPU by tests/golden/make_stream_digests.py
+        want = int(known["digest"])
     else:
         want = orc.cc_stream(G.generate_host(cfg), [0, E], V, partitions=8, threads=8)["digest"][0]
     print(f"{wl}: E={E} V={V} oracle digest {'cached' if known else f'in {time.time() - t:.1f}s'}", flush=True)
