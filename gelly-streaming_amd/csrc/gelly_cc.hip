@@ -2113,6 +2113,12 @@ int gcc_forest_capacity(gcc_forest* h, uint32_t* id_capacity) {
     return GCC_OK;
 }
 
+int gcc_forest_device(gcc_forest* h, int* device) {
+    CHECK_ARG(h && device, "null argument");
+    *device = h->device;
+    return GCC_OK;
+}
+
 int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent) {
     CHECK_ARG(h && d_parent, "null argument");
     DeviceGuard g(h->device);

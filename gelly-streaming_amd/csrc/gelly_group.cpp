@@ -1,0 +1,390 @@
+// gelly_group.cpp — the cross-GPU merge of the partial forests behind the C ABI (include/gelly_cc.h, "group").
+//
+// Reference: SummaryBulkAggregation.run ships every partition's partial DisjointSet, Kryo-serialised, to ONE task —
+// timeWindowAll(t).reduce(CombineCC) — and the parallelism-1 Merger folds it into the running summary
+// (…/SummaryBulkAggregation.java:81-83, …/library/ConnectedComponents.java:116-125, …/SummaryAggregation.java:107-119).
+//
+// Here every GPU keeps a full-range forest. A merge compresses each forest and encodes it as the compact message of
+// include/gelly_cc.h (header, bitmap of the tracked giant, (v, label) list of the other seen ids), ONE RCCL
+// all_gather over xGMI moves every message to every GPU, and each GPU absorbs the P-1 others in one launch
+// (gcc_forest_absorb_many) and compresses: every GPU then holds the global partition, with no serial bottleneck.
+// The list capacity is speculative (the last merge's need x 1.5); the gathered headers say whether some list did
+// not fit, and then the exchange is repeated larger — exact, since union is idempotent. When the compact form is
+// not smaller than the label array (no dominant component) the label arrays themselves are all-gathered.
+//
+// Built only on the public C ABI of the forest (encode / absorb / labels / merge_labels / compress / stream) plus
+// HIP and RCCL. RCCL is resolved at run time with dlopen("librccl.so.1"): a process that already mapped one (torch
+// does) shares it, so there is exactly one RCCL per process.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "abi_common.h"
+#include "gelly_cc.h"
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+namespace {
+
+struct Rccl {
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+    std::string error;
+};
+
+Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            r.error = std::string("dlopen librccl.so.1: ") + dlerror();
+            return;
+        }
+        auto sym = [&](const char* n) {
+            void* p = dlsym(h, n);
+            if (!p && r.error.empty()) r.error = std::string("dlsym ") + n;
+            return p;
+        };
+        r.GetUniqueId = (decltype(r.GetUniqueId))sym("ncclGetUniqueId");
+        r.CommInitRank = (decltype(r.CommInitRank))sym("ncclCommInitRank");
+        r.CommInitAll = (decltype(r.CommInitAll))sym("ncclCommInitAll");
+        r.CommDestroy = (decltype(r.CommDestroy))sym("ncclCommDestroy");
+        r.AllGather = (decltype(r.AllGather))sym("ncclAllGather");
+        r.GroupStart = (decltype(r.GroupStart))sym("ncclGroupStart");
+        r.GroupEnd = (decltype(r.GroupEnd))sym("ncclGroupEnd");
+        r.GetErrorString = (decltype(r.GetErrorString))sym("ncclGetErrorString");
+    });
+    return r;
+}
+
+int rccl_ready() {
+    Rccl& r = rccl();
+    if (!r.error.empty()) return gcc_set_err(GCC_E_NODEV, "RCCL unavailable: %s", r.error.c_str());
+    return GCC_OK;
+}
+
+#define NCCL_TRY(expr)                                                                                     \
+    do {                                                                                                   \
+        ncclResult_t r_ = (expr);                                                                          \
+        if (r_ != ncclSuccess)                                                                             \
+            return gcc_set_err(GCC_E_HIP, "%s failed: %s", #expr, rccl().GetErrorString(r_));              \
+    } while (0)
+
+#define ABI_TRY(expr)          \
+    do {                       \
+        int rc_ = (expr);      \
+        if (rc_) return rc_;   \
+    } while (0)
+
+u64 round16(u64 x) { return (x + 15) / 16 * 16; }
+
+}  // namespace
+
+// One rank's communicator (one per GPU) plus the merge's buffers, which it owns.
+struct gcc_comm {
+    ncclComm_t comm = nullptr;
+    int device = 0, nranks = 1, rank = 0;
+    void* d_send = nullptr;
+    u64 send_bytes = 0;
+    void* d_recv = nullptr;
+    u64 recv_bytes = 0;
+    u32* h_hdr = nullptr;  // pinned: the gathered headers (4 u32 per rank)
+    u64 cap_others = 0;    // the speculative list capacity (grows on overflow, shrinks slowly)
+    bool prefer_labels = false;
+    u64 last_bytes = 0;    // bytes each rank contributed to the last merge's all_gather
+    int last_rounds = 0;
+};
+
+namespace {
+
+int ensure(void*& p, u64& have, u64 need) {
+    if (have >= need) return GCC_OK;
+    if (p) HIP_TRY(hipFree(p));
+    p = nullptr;
+    have = 0;
+    HIP_TRY(hipMalloc(&p, (size_t)need));
+    have = need;
+    return GCC_OK;
+}
+
+int forest_info(gcc_forest* h, int* dev, u32* V, hipStream_t* s) {
+    ABI_TRY(gcc_forest_device(h, dev));
+    ABI_TRY(gcc_forest_capacity(h, V));
+    void* sp = nullptr;
+    ABI_TRY(gcc_forest_get_stream(h, &sp));
+    *s = (hipStream_t)sp;
+    return GCC_OK;
+}
+
+// The label-array exchange (no dominant component): all_gather of the canonical labels, absorb the others.
+int merge_labels_rccl(gcc_forest* h, gcc_comm* c, u32 V, hipStream_t st) {
+    const u32* lab = nullptr;
+    ABI_TRY(gcc_forest_labels_device(h, &lab));
+    ABI_TRY(ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * V * sizeof(u32)));
+    NCCL_TRY(rccl().AllGather(lab, c->d_recv, V, ncclUint32, c->comm, st));
+    for (int p = 0; p < c->nranks; ++p)
+        if (p != c->rank)
+            ABI_TRY(gcc_forest_merge_labels_device(h, static_cast<const u32*>(c->d_recv) + (u64)p * V, V));
+    ABI_TRY(gcc_forest_compress(h));
+    c->last_bytes = 4ull * V;
+    return GCC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gcc_comm_unique_id(void* id_out) {
+    CHECK_ARG(id_out, "id_out is null");
+    ABI_TRY(rccl_ready());
+    ncclUniqueId id;
+    NCCL_TRY(rccl().GetUniqueId(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+    return GCC_OK;
+}
+
+int gcc_comm_init(int device, int nranks, int rank, const void* id, gcc_comm** out) {
+    CHECK_ARG(out && id, "null argument");
+    *out = nullptr;
+    CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "rank out of range");
+    ABI_TRY(gcc_check_device(device));
+    ABI_TRY(rccl_ready());
+    DeviceGuard g(device);
+    gcc_comm* c = new gcc_comm();
+    c->device = device;
+    c->nranks = nranks;
+    c->rank = rank;
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    ncclResult_t r = rccl().CommInitRank(&c->comm, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return gcc_set_err(GCC_E_HIP, "ncclCommInitRank: %s", rccl().GetErrorString(r));
+    }
+    *out = c;
+    return GCC_OK;
+}
+
+int gcc_comm_init_all(int ndev, const int* devices, gcc_comm** comms_out) {
+    CHECK_ARG(ndev >= 1 && devices && comms_out, "null argument");
+    for (int i = 0; i < ndev; ++i) ABI_TRY(gcc_check_device(devices[i]));
+    ABI_TRY(rccl_ready());
+    std::vector<ncclComm_t> cs(ndev);
+    NCCL_TRY(rccl().CommInitAll(cs.data(), ndev, devices));
+    for (int i = 0; i < ndev; ++i) {
+        gcc_comm* c = new gcc_comm();
+        c->comm = cs[i];
+        c->device = devices[i];
+        c->nranks = ndev;
+        c->rank = i;
+        comms_out[i] = c;
+    }
+    return GCC_OK;
+}
+
+int gcc_comm_destroy(gcc_comm* c) {
+    if (!c) return GCC_OK;
+    DeviceGuard g(c->device);
+    if (c->d_send) (void)hipFree(c->d_send);
+    if (c->d_recv) (void)hipFree(c->d_recv);
+    if (c->h_hdr) (void)hipHostFree(c->h_hdr);
+    if (c->comm) (void)rccl().CommDestroy(c->comm);
+    delete c;
+    return GCC_OK;
+}
+
+int gcc_comm_info(gcc_comm* c, int* nranks, int* rank, uint64_t* last_bytes) {
+    CHECK_ARG(c, "null comm");
+    if (nranks) *nranks = c->nranks;
+    if (rank) *rank = c->rank;
+    if (last_bytes) *last_bytes = c->last_bytes;
+    return GCC_OK;
+}
+
+// Collective: every rank calls it with its forest (same id_capacity everywhere); afterwards every rank's forest is
+// the union of all of them, compressed. Synchronises the forest's stream (it reads the gathered headers).
+int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
+    CHECK_ARG(h && c, "null argument");
+    int dev;
+    u32 V;
+    hipStream_t st;
+    ABI_TRY(forest_info(h, &dev, &V, &st));
+    CHECK_ARG(dev == c->device, "forest and communicator are on different devices");
+    DeviceGuard g(dev);
+    if (c->nranks == 1) return gcc_forest_compress(h);
+    if (!c->h_hdr) HIP_TRY(hipHostMalloc((void**)&c->h_hdr, (size_t)c->nranks * 16, hipHostMallocDefault));
+    if (c->cap_others == 0) c->cap_others = std::max<u64>(1024, V / 64);
+    c->last_rounds = 0;
+    while (!c->prefer_labels) {
+        const u64 cap = c->cap_others;
+        const u64 size = round16(gcc_msg_bytes(V, cap));
+        if (size >= 4ull * V) {  // the compact form does not pay: labels from now on (exact after partial rounds)
+            c->prefer_labels = true;
+            break;
+        }
+        ABI_TRY(ensure(c->d_send, c->send_bytes, size));
+        ABI_TRY(ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * size));
+        ABI_TRY(gcc_forest_encode(h, c->d_send, cap));
+        NCCL_TRY(rccl().AllGather(c->d_send, c->d_recv, (size_t)size, ncclUint8, c->comm, st));
+        ABI_TRY(gcc_forest_absorb_many(h, c->d_recv, size, (u32)c->nranks, (u32)c->rank, cap));
+        HIP_TRY(hipMemcpy2DAsync(c->h_hdr, 16, c->d_recv, (size_t)size, 16, (size_t)c->nranks, hipMemcpyDeviceToHost, st));
+        ABI_TRY(gcc_forest_compress(h));
+        HIP_TRY(hipStreamSynchronize(st));
+        ++c->last_rounds;
+        c->last_bytes = size;
+        u64 nmax = 0;
+        for (int p = 0; p < c->nranks; ++p) nmax = std::max<u64>(nmax, c->h_hdr[4 * p + 1]);
+        if (nmax <= cap) {
+            if (4 * nmax < cap && cap > 1024) c->cap_others = std::max<u64>({1024, 3 * nmax / 2, cap / 2});
+            return GCC_OK;
+        }
+        c->cap_others = std::max<u64>(3 * nmax / 2, 2 * cap);  // some list did not fit: again, larger
+    }
+    ++c->last_rounds;
+    return merge_labels_rccl(h, c, V, st);
+}
+
+// Single process, n forests (SummaryTreeReduce's partials, or one forest per GPU of a process that drives several
+// GPUs): every forest := the union of all n. Forests on ONE device exchange their messages through one device
+// buffer (no RCCL); forests on different devices need comms from gcc_comm_init_all (comms[i] for hs[i]).
+int gcc_group_merge(gcc_forest** hs, int n, gcc_comm** comms) {
+    CHECK_ARG(hs && n >= 1, "null argument");
+    std::vector<int> dev(n);
+    std::vector<u32> V(n);
+    std::vector<hipStream_t> st(n);
+    for (int i = 0; i < n; ++i) {
+        CHECK_ARG(hs[i], "null forest");
+        ABI_TRY(forest_info(hs[i], &dev[i], &V[i], &st[i]));
+        CHECK_ARG(V[i] == V[0], "forests of one group need the same id_capacity");
+    }
+    if (n == 1) return gcc_forest_compress(hs[0]);
+    const bool one_device = std::all_of(dev.begin(), dev.end(), [&](int d) { return d == dev[0]; });
+    if (!one_device) {
+        CHECK_ARG(comms, "forests on several devices need comms (gcc_comm_init_all)");
+        for (int i = 0; i < n; ++i)
+            CHECK_ARG(comms[i] && comms[i]->device == dev[i] && comms[i]->rank == i && comms[i]->nranks == n,
+                      "comms[i] must be rank i of an n-rank group on forest i's device");
+        // one grouped launch of every rank's collective (a single thread drives all of them)
+        ABI_TRY(rccl_ready());
+        u64 cap = std::max<u64>(1024, V[0] / 64);
+        for (int round = 0;; ++round) {
+            const u64 size = round16(gcc_msg_bytes(V[0], cap));
+            const bool labels = size >= 4ull * V[0];
+            for (int i = 0; i < n; ++i) {
+                DeviceGuard g(dev[i]);
+                gcc_comm* c = comms[i];
+                if (!c->h_hdr) HIP_TRY(hipHostMalloc((void**)&c->h_hdr, (size_t)n * 16, hipHostMallocDefault));
+                if (labels) {
+                    ABI_TRY(ensure(c->d_recv, c->recv_bytes, (u64)n * V[0] * sizeof(u32)));
+                } else {
+                    ABI_TRY(ensure(c->d_send, c->send_bytes, size));
+                    ABI_TRY(ensure(c->d_recv, c->recv_bytes, (u64)n * size));
+                    ABI_TRY(gcc_forest_encode(hs[i], c->d_send, cap));
+                }
+            }
+            std::vector<const u32*> lab(n, nullptr);
+            if (labels)
+                for (int i = 0; i < n; ++i) ABI_TRY(gcc_forest_labels_device(hs[i], &lab[i]));
+            NCCL_TRY(rccl().GroupStart());
+            for (int i = 0; i < n; ++i) {
+                gcc_comm* c = comms[i];
+                ncclResult_t r = labels ? rccl().AllGather(lab[i], c->d_recv, V[0], ncclUint32, c->comm, st[i])
+                                        : rccl().AllGather(c->d_send, c->d_recv, (size_t)size, ncclUint8, c->comm, st[i]);
+                if (r != ncclSuccess) {
+                    (void)rccl().GroupEnd();
+                    return gcc_set_err(GCC_E_HIP, "ncclAllGather: %s", rccl().GetErrorString(r));
+                }
+            }
+            NCCL_TRY(rccl().GroupEnd());
+            u64 nmax = 0;
+            for (int i = 0; i < n; ++i) {
+                DeviceGuard g(dev[i]);
+                gcc_comm* c = comms[i];
+                if (labels) {
+                    for (int p = 0; p < n; ++p)
+                        if (p != i)
+                            ABI_TRY(gcc_forest_merge_labels_device(
+                                hs[i], static_cast<const u32*>(c->d_recv) + (u64)p * V[0], V[0]));
+                } else {
+                    ABI_TRY(gcc_forest_absorb_many(hs[i], c->d_recv, size, (u32)n, (u32)i, cap));
+                    HIP_TRY(hipMemcpy2DAsync(c->h_hdr, 16, c->d_recv, (size_t)size, 16, (size_t)n,
+                                             hipMemcpyDeviceToHost, st[i]));
+                }
+                ABI_TRY(gcc_forest_compress(hs[i]));
+            }
+            for (int i = 0; i < n; ++i) {
+                DeviceGuard g(dev[i]);
+                HIP_TRY(hipStreamSynchronize(st[i]));
+                if (!labels)
+                    for (int p = 0; p < n; ++p) nmax = std::max<u64>(nmax, comms[i]->h_hdr[4 * p + 1]);
+            }
+            if (labels || nmax <= cap) return GCC_OK;
+            cap = std::max<u64>(3 * nmax / 2, 2 * cap);
+        }
+    }
+    // one device: the messages of all n forests in one buffer, each forest absorbs the others
+    DeviceGuard g(dev[0]);
+    struct Buf {
+        void* d = nullptr;
+        u64 bytes = 0;
+        u32* hdr = nullptr;
+        ~Buf() {
+            if (d) (void)hipFree(d);
+            if (hdr) (void)hipHostFree(hdr);
+        }
+    } buf;
+    HIP_TRY(hipHostMalloc((void**)&buf.hdr, (size_t)n * 16, hipHostMallocDefault));
+    std::vector<hipEvent_t> ev(n, nullptr);
+    struct Evs {
+        std::vector<hipEvent_t>& e;
+        ~Evs() {
+            for (auto x : e)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } evs{ev};
+    for (int i = 0; i < n; ++i) HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    u64 cap = std::max<u64>(1024, V[0] / 64);
+    while (true) {
+        const u64 size = round16(gcc_msg_bytes(V[0], cap));
+        if (size >= 4ull * V[0]) {  // labels: CombineCC pairwise into forest 0, then forest 0's partition to all
+            for (int i = 1; i < n; ++i) ABI_TRY(gcc_forest_merge(hs[0], hs[i]));
+            ABI_TRY(gcc_forest_compress(hs[0]));
+            for (int i = 1; i < n; ++i) ABI_TRY(gcc_forest_merge(hs[i], hs[0]));
+            for (int i = 0; i < n; ++i) ABI_TRY(gcc_forest_sync(hs[i]));
+            return GCC_OK;
+        }
+        ABI_TRY(ensure(buf.d, buf.bytes, (u64)n * size));
+        for (int i = 0; i < n; ++i) {
+            ABI_TRY(gcc_forest_encode(hs[i], static_cast<char*>(buf.d) + (u64)i * size, cap));
+            HIP_TRY(hipEventRecord(ev[i], st[i]));
+        }
+        for (int i = 0; i < n; ++i) {
+            for (int j = 0; j < n; ++j) HIP_TRY(hipStreamWaitEvent(st[i], ev[j], 0));  // every message written
+            ABI_TRY(gcc_forest_absorb_many(hs[i], buf.d, size, (u32)n, (u32)i, cap));
+            ABI_TRY(gcc_forest_compress(hs[i]));
+        }
+        HIP_TRY(hipMemcpy2DAsync(buf.hdr, 16, buf.d, (size_t)size, 16, (size_t)n, hipMemcpyDeviceToHost, st[0]));
+        for (int i = 0; i < n; ++i) HIP_TRY(hipStreamSynchronize(st[i]));  // also: no encode overwrites a message early
+        u64 nmax = 0;
+        for (int p = 0; p < n; ++p) nmax = std::max<u64>(nmax, buf.hdr[4 * p + 1]);
+        if (nmax <= cap) return GCC_OK;
+        cap = std::max<u64>(3 * nmax / 2, 2 * cap);
+    }
+}
+
+}  // extern "C"

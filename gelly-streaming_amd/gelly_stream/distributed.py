@@ -17,7 +17,9 @@ RCCL send/recv with rank ^ 2^r for a power-of-two world, all_gather otherwise.
 """
 from __future__ import annotations
 
-from typing import Optional, Protocol
+import ctypes
+import os
+from typing import Optional, Protocol, Sequence
 
 
 class ExchangeForest(Protocol):
@@ -79,6 +81,84 @@ class TorchDisjointSet:
         return getattr(self.ds, name)
 
 
+class RcclComm:
+    """One rank's RCCL communicator behind the C ABI (gcc_comm_*, csrc/gelly_group.cpp): the merge of
+    timeWindowAll(t).reduce(CombineCC) + Merger (SummaryBulkAggregation.java:81-83) as ONE all_gather of compact
+    forest messages over xGMI, run entirely by libgelly_cc (no torch collective on the data path)."""
+
+    ID_BYTES = 128  # GCC_COMM_ID_BYTES
+
+    def __init__(self, device: int, nranks: int, rank: int, uid: bytes, _handle=None):
+        from .native import call
+
+        self.device, self.nranks, self.rank = int(device), int(nranks), int(rank)
+        if _handle is not None:
+            self._h = _handle
+            return
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), self.ID_BYTES)
+        call("gcc_comm_init", self.device, self.nranks, self.rank, buf, ctypes.byref(h))
+        self._h = h
+
+    @classmethod
+    def unique_id(cls) -> bytes:
+        from .native import call
+
+        buf = ctypes.create_string_buffer(cls.ID_BYTES)
+        call("gcc_comm_unique_id", buf)
+        return buf.raw
+
+    @classmethod
+    def init_all(cls, devices: Sequence[int]) -> list["RcclComm"]:
+        """One process driving several GPUs: rank i on devices[i] (ncclCommInitAll)."""
+        from .native import call
+
+        n = len(devices)
+        devs = (ctypes.c_int * n)(*devices)
+        hs = (ctypes.c_void_p * n)()
+        call("gcc_comm_init_all", n, devs, hs)
+        return [cls(d, n, i, b"", _handle=ctypes.c_void_p(hs[i])) for i, d in enumerate(devices)]
+
+    def merge(self, ds) -> None:
+        """Collective: ds (a DisjointSet on this rank's device) := the union of every rank's forest."""
+        from .native import call
+
+        call("gcc_forest_group_merge", ds.handle, self._h)
+
+    def last_bytes(self) -> int:
+        from .native import call
+
+        b = ctypes.c_uint64()
+        call("gcc_comm_info", self._h, None, None, ctypes.byref(b))
+        return b.value
+
+    def close(self) -> None:
+        from .native import call
+
+        if getattr(self, "_h", None):
+            call("gcc_comm_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def group_merge(forests: Sequence, comms: Optional[Sequence[RcclComm]] = None) -> None:
+    """Single process: every forest := the union of all of them (gcc_group_merge). Forests on one device need no
+    comms; forests on several devices need RcclComm.init_all over their devices (comms[i] for forests[i])."""
+    from .native import call
+
+    n = len(forests)
+    hs = (ctypes.c_void_p * n)(*[f.handle.value for f in forests])
+    cs = None if comms is None else (ctypes.c_void_p * n)(*[c._h.value for c in comms])
+    call("gcc_group_merge", hs, n, cs)
+    for f in forests:
+        f._dirty()
+
+
 def _round16(n: int) -> int:
     return (int(n) + 15) // 16 * 16
 
@@ -87,7 +167,10 @@ class ForestGroup:
     """Cross-rank merge of one forest per rank (mode "auto": compact all_gather, label exchange fallback;
     "labels": always exchange label arrays)."""
 
-    def __init__(self, group=None, mode: str = "auto"):
+    def __init__(self, group=None, mode: str = "auto", transport: str = "auto", device: Optional[int] = None):
+        """transport "rccl": the merge runs in libgelly_cc over its own RCCL communicator (gcc_forest_group_merge);
+        "torch": the same protocol driven from Python over torch.distributed (gloo rehearsals on CPU); "auto": rccl
+        when the group's backend is nccl (= RCCL) unless GELLY_MERGE=torch."""
         import torch.distributed as dist
 
         if mode not in ("auto", "labels"):
@@ -97,6 +180,18 @@ class ForestGroup:
         self.mode = mode
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.comm: Optional[RcclComm] = None
+        if transport == "auto":
+            backend = str(dist.get_backend(group)).lower()
+            transport = "rccl" if backend == "nccl" and os.environ.get("GELLY_MERGE", "") != "torch" else "torch"
+        if transport == "rccl" and mode == "auto":
+            import torch
+
+            dev = torch.cuda.current_device() if device is None else int(device)
+            uid = [RcclComm.unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(uid, src=self._global(0), group=group)  # bootstrap bytes only
+            self.comm = RcclComm(dev, self.world, self.rank, uid[0])
+        self.transport = transport
         self._recv = None
         self._gather = None
         self._cap = 0          # list capacity of the message buffer (grows, never shrinks)
@@ -125,6 +220,10 @@ class ForestGroup:
 
     def merge_forest(self, forest: ExchangeForest) -> None:
         """forest := union of every rank's forest (collective: every rank must call it)."""
+        if self.comm is not None:  # the whole merge inside libgelly_cc, over RCCL
+            self.comm.merge(forest.ds if hasattr(forest, "ds") else forest)
+            self.last = {"compact": True, "bytes": self.comm.last_bytes(), "transport": "rccl"}
+            return
         forest.compress()
         if self.world == 1:
             return

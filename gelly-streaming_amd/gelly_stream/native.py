@@ -63,6 +63,15 @@ _SIGS = {
     "gcc_forest_set_stream": (c_int, [c_void_p, c_void_p, c_int]),
     "gcc_forest_get_stream": (c_int, [c_void_p, POINTER(c_void_p)]),
     "gcc_forest_capacity": (c_int, [c_void_p, POINTER(c_uint32)]),
+    "gcc_forest_device": (c_int, [c_void_p, POINTER(c_int)]),
+    # cross-GPU group merge over RCCL (gelly_group.cpp)
+    "gcc_comm_unique_id": (c_int, [c_void_p]),
+    "gcc_comm_init": (c_int, [c_int, c_int, c_int, c_void_p, POINTER(c_void_p)]),
+    "gcc_comm_init_all": (c_int, [c_int, c_void_p, c_void_p]),
+    "gcc_comm_destroy": (c_int, [c_void_p]),
+    "gcc_comm_info": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_uint64)]),
+    "gcc_forest_group_merge": (c_int, [c_void_p, c_void_p]),
+    "gcc_group_merge": (c_int, [c_void_p, c_int, c_void_p]),
     "gcc_forest_device_ptr": (c_int, [c_void_p, POINTER(c_void_p)]),
     "gcc_forest_reset": (c_int, [c_void_p]),
     "gcc_forest_union": (c_int, [c_void_p, c_uint32, c_uint32]),

@@ -91,6 +91,7 @@ int gcc_forest_destroy(gcc_forest* h);
 int gcc_forest_set_stream(gcc_forest* h, void* hip_stream, int use_own);
 int gcc_forest_get_stream(gcc_forest* h, void** hip_stream);
 int gcc_forest_capacity(gcc_forest* h, uint32_t* id_capacity);
+int gcc_forest_device(gcc_forest* h, int* device);
 /* current forest buffer (= labels after compress); the caller may WRITE through it, so every cached view of the
  * forest is dropped (the next read compresses again) */
 int gcc_forest_device_ptr(gcc_forest* h, uint32_t** d_parent);
@@ -142,6 +143,27 @@ int gcc_forest_absorb(gcc_forest* h, const void* d_msg, uint64_t cap_others);
  * the receive side of the all_gather; stride_bytes >= gcc_msg_bytes(id_capacity, cap_others), 16-B aligned */
 int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_bytes, uint32_t count, uint32_t skip,
                            uint64_t cap_others);
+
+/* ---- cross-GPU group merge (gelly_group.cpp): replaces timeWindowAll(t).reduce(CombineCC) + the parallelism-1
+ * Merger (…/SummaryBulkAggregation.java:81-83, …/SummaryAggregation.java:107-119). One communicator per GPU over
+ * RCCL (xGMI); every rank's forest becomes the union of all ranks' forests — ONE all_gather of the compact messages
+ * above (label arrays when no component dominates), each rank absorbing the others itself. RCCL is loaded at run
+ * time (dlopen librccl.so.1; a process that already mapped one, e.g. torch's, shares it). */
+typedef struct gcc_comm gcc_comm;
+#define GCC_COMM_ID_BYTES 128 /* = the RCCL unique id */
+/* rank 0 creates the id and hands its bytes to every rank over any channel (torch.distributed, the JVM, a file) */
+int gcc_comm_unique_id(void* id_out);
+int gcc_comm_init(int device, int nranks, int rank, const void* id, gcc_comm** out); /* one process per GPU */
+int gcc_comm_init_all(int ndev, const int* devices, gcc_comm** comms_out);           /* one process, ndev GPUs */
+int gcc_comm_destroy(gcc_comm* c);
+/* nranks, rank, and the bytes each rank contributed to the last merge's all_gather (any may be NULL) */
+int gcc_comm_info(gcc_comm* c, int* nranks, int* rank, uint64_t* last_bytes);
+/* collective over the communicator's ranks (every rank calls it with its forest, same id_capacity); synchronises
+ * the forest's stream. Afterwards every rank's forest holds the global partition, compressed. */
+int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c);
+/* single process: hs[0..n) := their union. Forests on one device need no comms (NULL); forests on several devices
+ * need comms[i] = rank i of a gcc_comm_init_all group on hs[i]'s device. Synchronises every forest's stream. */
+int gcc_group_merge(gcc_forest** hs, int n, gcc_comm** comms);
 
 /* ---- BipartitenessCheck's summary: Candidates (…/summaries/Candidates.java:27-197) as a signed forest ----
  * BipartitenessCheck(mergeWindowTime) = SummaryBulkAggregation(updateFunction, combineFunction, new Candidates(true),

@@ -80,3 +80,99 @@ def test_forest_group_ranks_share_one_gpu(mode, world):
     for p in procs:
         p.join(timeout=60)
     assert sorted(results) == [(r, -1, "ok") for r in range(world)], results
+
+
+# ---- the group merge behind the C ABI (csrc/gelly_group.cpp) ----
+def _windows_vs_oracle(cfg, starts, P, merge):
+    import oracle as orc
+    import torch
+    from gelly_stream import DisjointSet
+    from gelly_stream import generators as G
+
+    E, V = cfg.info()
+    want = orc.cc_stream(G.generate_host(cfg), starts, V, partitions=P, threads=2, want_labels=True)["labels"]
+    d = torch.empty(2 * E, dtype=torch.int32, device="cuda:0")
+    G.generate_device(cfg, 0, E, d.data_ptr(), 0)
+    torch.cuda.synchronize()
+    forests = [DisjointSet(V) for _ in range(P)]
+    for w in range(len(starts) - 1):
+        b, e = int(starts[w]), int(starts[w + 1])
+        for r, ds in enumerate(forests):  # rank r folds its contiguous 1/P of the window (bench.py's partitioning)
+            lo, hi = b + (e - b) * r // P, b + (e - b) * (r + 1) // P
+            ds.fold_device(d.data_ptr() + 8 * lo, hi - lo)
+        merge(forests)
+        for r, ds in enumerate(forests):
+            got = ds.labels()
+            assert np.array_equal(got, want[w]), (w, r, int(np.flatnonzero(got != want[w])[0]))
+    for ds in forests:
+        ds.close()
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_c_abi_group_merge_one_device(P):
+    """gcc_group_merge over P forests on one GPU: the compact message all-gather through one device buffer, each
+    forest absorbing the others (the RCCL path's protocol without the transport). R-MAT: one dominant component."""
+    from gelly_stream import generators as G
+    from gelly_stream.distributed import group_merge
+
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=17, n_edges=1 << 20, seed=0x6770)
+    starts = np.asarray([0, 1000, 1 << 17, 1 << 19, 1 << 20], dtype=np.uint64)
+    _windows_vs_oracle(cfg, starts, P, group_merge)
+
+
+def test_c_abi_group_merge_retry_and_label_fallback():
+    """G(n, m) near the threshold: no dominant component, so the lists overflow the speculative capacity (a repeat
+    round, exact because union is idempotent) until the compact form stops paying and labels are exchanged."""
+    from gelly_stream import generators as G
+    from gelly_stream.distributed import group_merge
+
+    cfg = G.scaled(G.CONFIGS["c3_gnm24"], n_vertices=1 << 18, n_edges=1 << 17, seed=0x3131)
+    starts = np.asarray([0, 1 << 10, 1 << 15, 1 << 17], dtype=np.uint64)
+    _windows_vs_oracle(cfg, starts, 3, group_merge)
+
+
+def test_rccl_comm_single_rank():
+    """The RCCL transport loads (dlopen librccl.so.1, shared with torch's) and a 1-rank communicator merges (=
+    compresses); gcc_forest_group_merge checks the forest's device against the communicator's."""
+    from gelly_stream import DisjointSet
+    from gelly_stream.distributed import RcclComm
+
+    comm = RcclComm(0, 1, 0, RcclComm.unique_id())
+    ds = DisjointSet(1 << 12)
+    ds.fold(np.array([[5, 6], [6, 9], [100, 101]], dtype=np.uint32))
+    comm.merge(ds)
+    ds._dirty()
+    assert ds.find(9) == 5 and ds.find(101) == 100 and ds.size() == 5
+    ds.close()
+    comm.close()
+
+
+def test_c_abi_group_merge_two_devices():
+    """Two forests on two GPUs merged through gcc_comm_init_all + gcc_group_merge (RCCL): needs >= 2 GPUs."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (the driver's multi-GPU node)")
+    import oracle as orc
+    from gelly_stream import DisjointSet
+    from gelly_stream import generators as G
+    from gelly_stream.distributed import RcclComm, group_merge
+
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=16, n_edges=1 << 19)
+    E, V = cfg.info()
+    pairs = G.generate_host(cfg)
+    want = orc.cc_stream(pairs, [0, E], V, want_labels=True)["labels"][0]
+    comms = RcclComm.init_all([0, 1])
+    a, b = DisjointSet(V, 0), DisjointSet(V, 1)
+    a.fold(pairs[: E // 2])
+    b.fold(pairs[E // 2:])
+    group_merge([a, b], comms)
+    assert np.array_equal(a.labels(), want) and np.array_equal(b.labels(), want)
+    # and DisjointSet.merge across the two devices (CombineCC with a peer copy)
+    c = DisjointSet(V, 1)
+    c.merge(a)
+    assert np.array_equal(c.labels(), want)
+    for x in (a, b, c):
+        x.close()
+    for x in comms:
+        x.close()
