@@ -2427,6 +2427,125 @@ int gcc_forest_absorb(gcc_forest* h, const void* d_msg, uint64_t cap_others) {
     return gcc_forest_absorb_many(h, d_msg, 0, 1, UINT32_MAX, cap_others);
 }
 
+// ---- serialized summary (Merger.snapshotState / restoreState; the bytes Kryo ships for a DisjointSet) ----------
+// Layout (include/gelly_cc.h): a 32-byte header {magic, version, id_capacity, kind, n_seen, payload bytes}, then
+// kind 1: n_seen (v, label) u32 pairs in id order; kind 2: the compact merge message with cap_others = its count.
+// serialize picks the smaller form (the message when one component dominates: ~V/8 bytes + the other ids).
+struct SerHeader {
+    u32 magic, version, id_capacity, kind;
+    u64 n_seen, payload;
+};
+static_assert(sizeof(SerHeader) == GCC_SER_HEADER_BYTES, "serialized header");
+
+static int ser_plan(gcc_forest* h, u32* kind, u64* n_seen, u64* n_others, u64* payload) {
+    unsigned long long c[2];
+    int rc = counts(h, c);  // flush + exact #seen
+    if (rc) return rc;
+    *n_seen = c[0];
+    rc = compress_async(h);
+    if (rc) return rc;
+    // the message's true list length: an encode with capacity 0 still counts every other id into its header
+    const u64 hdr_only = gcc_msg_bytes(h->cap, 0);
+    u8* tmp = nullptr;
+    HIP_TRY(hipMalloc((void**)&tmp, (size_t)hdr_only));
+    rc = gcc_forest_encode(h, tmp, 0);
+    u32 hdr[4] = {0, 0, 0, 0};
+    if (!rc) {
+        hipError_t e = hipMemcpyAsync(hdr, tmp, sizeof(hdr), hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) rc = set_err(GCC_E_HIP, "serialize: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(tmp);
+    if (rc) return rc;
+    *n_others = hdr[1];
+    const u64 msg = gcc_msg_bytes(h->cap, *n_others), pairs = 8ull * *n_seen;
+    *kind = (h->has_giant && msg < pairs) ? 2u : 1u;
+    *payload = *kind == 2 ? msg : pairs;
+    return GCC_OK;
+}
+
+int gcc_forest_serialized_size(gcc_forest* h, uint64_t* bytes) {
+    CHECK_ARG(h && bytes, "null argument");
+    DeviceGuard g(h->device);
+    u32 kind;
+    u64 n_seen, n_others, payload;
+    int rc = ser_plan(h, &kind, &n_seen, &n_others, &payload);
+    if (rc) return rc;
+    *bytes = GCC_SER_HEADER_BYTES + payload;
+    return GCC_OK;
+}
+
+int gcc_forest_serialize(gcc_forest* h, void* out, uint64_t size, uint64_t* written) {
+    CHECK_ARG(h && out, "null argument");
+    DeviceGuard g(h->device);
+    u32 kind;
+    u64 n_seen, n_others, payload;
+    int rc = ser_plan(h, &kind, &n_seen, &n_others, &payload);
+    if (rc) return rc;
+    if (size < GCC_SER_HEADER_BYTES + payload)
+        return set_err(GCC_E_INVALID, "serialize: buffer of %llu bytes, need %llu", (unsigned long long)size,
+                       (unsigned long long)(GCC_SER_HEADER_BYTES + payload));
+    SerHeader hd{GCC_SER_MAGIC, 1u, h->cap, kind, n_seen, payload};
+    std::memcpy(out, &hd, sizeof(hd));
+    u8* body = static_cast<u8*>(out) + GCC_SER_HEADER_BYTES;
+    if (kind == 2) {  // the message, straight from the device
+        u8* d = nullptr;
+        HIP_TRY(hipMalloc((void**)&d, (size_t)payload));
+        rc = gcc_forest_encode(h, d, n_others);
+        hipError_t e = hipSuccess;
+        if (!rc) e = hipMemcpyAsync(body, d, (size_t)payload, hipMemcpyDeviceToHost, h->stream);
+        if (!rc && e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        (void)hipFree(d);
+        if (rc) return rc;
+        if (e != hipSuccess) return set_err(GCC_E_HIP, "serialize: %s", hipGetErrorString(e));
+    } else {  // (v, label) of every seen id, in id order
+        rc = refresh_host(h);
+        if (rc) return rc;
+        u32* p = reinterpret_cast<u32*>(body);
+        u64 k = 0;
+        for (u32 v = 0; v < h->cap && k < n_seen; ++v)
+            if (h->host_labels[v] != UNSEEN) {
+                p[2 * k] = v;
+                p[2 * k + 1] = h->host_labels[v];
+                ++k;
+            }
+    }
+    if (written) *written = GCC_SER_HEADER_BYTES + payload;
+    return GCC_OK;
+}
+
+int gcc_forest_deserialize(gcc_forest* h, const void* in, uint64_t size) {
+    CHECK_ARG(h && in, "null argument");
+    CHECK_ARG(size >= GCC_SER_HEADER_BYTES, "serialized summary shorter than its header");
+    SerHeader hd;
+    std::memcpy(&hd, in, sizeof(hd));
+    CHECK_ARG(hd.magic == GCC_SER_MAGIC && hd.version == 1, "not a serialized gelly summary (magic / version)");
+    CHECK_ARG(hd.id_capacity <= h->cap, "serialized summary has a larger id range than the forest");
+    CHECK_ARG(size >= GCC_SER_HEADER_BYTES + hd.payload, "serialized summary truncated");
+    DeviceGuard g(h->device);
+    const u8* body = static_cast<const u8*>(in) + GCC_SER_HEADER_BYTES;
+    if (hd.kind == 1) {
+        CHECK_ARG(hd.payload == 8 * hd.n_seen, "serialized pairs: bad length");
+        return gcc_forest_fold_host(h, reinterpret_cast<const u32*>(body), hd.n_seen);  // ids validated there
+    }
+    CHECK_ARG(hd.kind == 2, "serialized summary: unknown kind");
+    CHECK_ARG(hd.id_capacity == h->cap, "a serialized message restores into a forest of the same id range only");
+    CHECK_ARG(hd.payload >= GCC_MSG_HEADER_BYTES, "serialized message: bad length");
+    u32 mh[4];
+    std::memcpy(mh, body, sizeof(mh));
+    const u64 n_others = mh[1];
+    CHECK_ARG(mh[2] == h->cap && hd.payload == gcc_msg_bytes(h->cap, n_others) &&
+                  (mh[0] == UNSEEN || mh[0] < h->cap),
+              "serialized message: inconsistent header");
+    u8* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, (size_t)hd.payload));
+    hipError_t e = hipMemcpyAsync(d, body, (size_t)hd.payload, hipMemcpyHostToDevice, h->stream);
+    int rc = e == hipSuccess ? gcc_forest_absorb(h, d, n_others) : set_err(GCC_E_HIP, "%s", hipGetErrorString(e));
+    if (!rc) rc = stream_sync_checked(h);  // the staging buffer is freed below
+    (void)hipFree(d);
+    return rc;
+}
+
 int gcc_forest_compress(gcc_forest* h) {
     CHECK_ARG(h, "null forest");
     DeviceGuard g(h->device);

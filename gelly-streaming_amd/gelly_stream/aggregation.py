@@ -87,12 +87,19 @@ class Merger(Generic[S]):
         return out
 
     def snapshotState(self) -> list:
-        """:127-130"""
-        return [self.summary]
+        """:127-130 — ListCheckpointed: the running summary in its serialized form (bytes) when it has one (a device
+        summary: DisjointSet.serialize, include/gelly_cc.h "serialized summary"), else the object itself."""
+        s = self.summary
+        return [s.serialize() if hasattr(s, "serialize") else s]
 
     def restoreState(self, state: list) -> None:
-        """:132-135"""
-        self.summary = state[0]
+        """:132-135 — a serialized summary is rebuilt into a fresh one from the initial-value factory."""
+        s = state[0] if state else None
+        if isinstance(s, (bytes, bytearray)):
+            fresh = self._initial()
+            fresh.deserialize(s)
+            s = fresh
+        self.summary = s
 
 
 class SummaryAggregation(ABC, Generic[S, T]):

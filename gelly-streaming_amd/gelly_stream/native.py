@@ -93,6 +93,9 @@ _SIGS = {
     "gcc_forest_size": (c_int, [c_void_p, POINTER(c_uint64)]),
     "gcc_forest_count_components": (c_int, [c_void_p, POINTER(c_uint64)]),
     "gcc_forest_import_pairs": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_forest_serialized_size": (c_int, [c_void_p, POINTER(c_uint64)]),
+    "gcc_forest_serialize": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "gcc_forest_deserialize": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_forest_enable_timing": (c_int, [c_void_p, c_int]),
     "gcc_forest_last_fold_ms": (c_int, [c_void_p, POINTER(c_float)]),
     "gcc_forest_fold_profile": (c_int, [c_void_p, c_char_p, c_uint64]),

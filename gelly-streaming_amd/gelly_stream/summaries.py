@@ -253,6 +253,29 @@ class DisjointSet:
         call("gcc_forest_import_pairs", self.handle, a.ctypes.data, a.size // 2)
         self._dirty()
 
+    def serialize(self) -> bytes:
+        """The summary's checkpoint / wire bytes (include/gelly_cc.h "serialized summary": (v, label) pairs, or the
+        compact merge message when one component dominates). Merger.snapshotState (SummaryAggregation.java:127-130)."""
+        n = c_uint64()
+        call("gcc_forest_serialized_size", self.handle, byref(n))
+        buf = ctypes.create_string_buffer(n.value)
+        w = c_uint64()
+        call("gcc_forest_serialize", self.handle, buf, n.value, byref(w))
+        return buf.raw[:w.value]
+
+    def deserialize(self, data: bytes) -> None:
+        """Fold a serialized summary into this one (into a fresh or reset forest: Merger.restoreState, :132-135)."""
+        call("gcc_forest_deserialize", self.handle, ctypes.c_char_p(bytes(data)), len(data))
+        self._dirty()
+
+    @classmethod
+    def from_bytes(cls, data: bytes, id_capacity: Optional[int] = None, device: int = 0) -> "DisjointSet":
+        """A new summary restored from serialize()'s bytes (the id range defaults to the serialized one)."""
+        cap = id_capacity if id_capacity is not None else int.from_bytes(bytes(data[8:12]), "little")
+        ds = cls(cap, device)
+        ds.deserialize(data)
+        return ds
+
     def snapshot_pairs(self) -> np.ndarray:
         """Serialisable state (Merger.snapshotState, SummaryAggregation.java:127-130): (v, label[v]) of seen v."""
         lab = self.labels()

@@ -195,6 +195,22 @@ int gcc_forest_count_components(gcc_forest* h, uint64_t* n_components);
 /* restore / deserialize: fold (key, parent) pairs (Merger.restoreState :132-135 + Kryo path) */
 int gcc_forest_import_pairs(gcc_forest* h, const uint32_t* pairs, uint64_t n_pairs);
 
+/* ---- serialized summary: the checkpoint / wire form of a DisjointSet (Merger.snapshotState / restoreState,
+ * …/SummaryAggregation.java:127-135, and the Kryo bytes a partial is shipped as, …/SummaryBulkAggregation.java:81).
+ * Little-endian bytes:
+ *   header (GCC_SER_HEADER_BYTES): u32 magic GCC_SER_MAGIC, u32 version 1, u32 id_capacity, u32 kind,
+ *                                  u64 n_seen (getMatches().size()), u64 payload bytes
+ *   kind 1 (pairs):   n_seen x {u32 v, u32 canonical label}, ascending v
+ *   kind 2 (message): the compact merge message above with cap_others = its n_others (a dominant component:
+ *                     ~id_capacity/8 bytes instead of 8 per seen id)
+ * serialize writes whichever is smaller into a HOST buffer (size from gcc_forest_serialized_size, which
+ * synchronises); deserialize folds a summary INTO h (restore = reset + deserialize: the same partition). */
+#define GCC_SER_MAGIC 0x53434347u /* "GCCS" */
+#define GCC_SER_HEADER_BYTES 32
+int gcc_forest_serialized_size(gcc_forest* h, uint64_t* bytes);
+int gcc_forest_serialize(gcc_forest* h, void* out, uint64_t size, uint64_t* written);
+int gcc_forest_deserialize(gcc_forest* h, const void* in, uint64_t size);
+
 /* ---- measurement: duration of the last fold launch (HIP events on the handle's stream) ---- */
 int gcc_forest_enable_timing(gcc_forest* h, int enable); /* 0 off, 1 events, 2 events + slow-edge counts */
 int gcc_forest_last_fold_ms(gcc_forest* h, float* ms);

@@ -213,3 +213,56 @@ def test_c4_share_strong_split_and_merge(torch_cuda):
         ds.close()
     del d
     torch_cuda.cuda.empty_cache()
+
+
+# ---- checkpoint / serialized summary (Merger.snapshotState / restoreState, SummaryAggregation.java:127-135) ----
+@pytest.mark.parametrize("kind,cfg_args", [
+    (2, ("c2_rmat20", {"scale": 18, "n_edges": 1 << 21, "seed": 0x5EED})),      # a dominant component: message
+    (1, ("c3_gnm24", {"n_vertices": 1 << 19, "n_edges": 1 << 18, "seed": 0x5EED})),  # none: (v, label) pairs
+])
+def test_checkpoint_restore_then_keep_folding(torch_cuda, kind, cfg_args):
+    """Fold windows; after every window snapshot the running summary (Merger.snapshotState -> bytes), restore it into
+    a fresh summary (Merger.restoreState), and keep folding BOTH: every window of both equals the oracle."""
+    from gelly_stream.aggregation import Merger
+    from gelly_stream.library import CombineCC
+
+    cfg = G.scaled(G.CONFIGS[cfg_args[0]], **cfg_args[1])
+    E, V = cfg.info()
+    pairs = G.generate_host(cfg)
+    starts = np.linspace(0, E, 6).astype(np.uint64)
+    want = orc.cc_stream(pairs, starts, V, partitions=2, threads=2)["digest"]
+    d = to_device(torch_cuda, pairs)
+    live = Merger(lambda: DisjointSet(V), CombineCC(), False)
+    restored = None
+    for w in range(len(starts) - 1):
+        b, e = int(starts[w]), int(starts[w + 1])
+        for m in (live, restored):
+            if m is None:
+                continue
+            part = DisjointSet(V)
+            part.fold_device(d.data_ptr() + 8 * b, e - b)
+            out = m.flatMap(part)
+            assert orc.label_digest(out.labels()) == int(want[w]), (w, m is restored)
+        state = live.snapshotState()
+        assert isinstance(state[0], bytes)
+        hdr = np.frombuffer(state[0][:32], dtype="<u4")
+        assert hdr[0] == 0x53434347 and hdr[1] == 1 and hdr[2] == V
+        if w == len(starts) - 2:
+            assert hdr[3] == kind, hdr  # the smaller form for this graph
+        restored = Merger(lambda: DisjointSet(V), CombineCC(), False)
+        restored.restoreState(state)
+        assert np.array_equal(restored.summary.labels(), live.summary.labels()), w
+
+
+def test_serialized_summary_rejects_bad_bytes():
+    ds = DisjointSet(1 << 10)
+    ds.fold(np.array([[1, 2], [3, 4]], dtype=np.uint32))
+    blob = ds.serialize()
+    with pytest.raises(GellyCCError):
+        DisjointSet(1 << 10).deserialize(b"\x00" * 40)  # bad magic
+    with pytest.raises(GellyCCError):
+        DisjointSet(1 << 10).deserialize(blob[:-4])  # truncated
+    with pytest.raises(GellyCCError):
+        DisjointSet(1 << 5).deserialize(blob)  # larger id range than the target
+    again = DisjointSet.from_bytes(blob)
+    assert again.find(2) == 1 and again.find(4) == 3 and again.size() == 4
