@@ -1,0 +1,49 @@
+// NOT COMPILED IN THIS IMAGE (no JDK): reference-side bridge, see gelly-streaming_amd/java/README.md
+package org.apache.flink.graph.streaming.gpu;
+
+import java.nio.ByteBuffer;
+
+/**
+ * JNI entry points over the C ABI of include/gelly_cc.h (glue: gelly-streaming_amd/java/jni/gcc_jni.c). Every
+ * method throws GccException when the C call returns a negative status. Handles are native pointers (long).
+ */
+final class Gcc {
+    static {
+        System.loadLibrary("gelly_cc_jni"); // links libgelly_cc.so (gfx950)
+    }
+
+    private Gcc() {}
+
+    /** gcc_forest_create: `new DisjointSet<>()` (DisjointSet.java:36-39), ids in [0, idCapacity). */
+    static native long create(int device, int idCapacity);
+
+    /** gcc_forest_destroy. */
+    static native void destroy(long h);
+
+    /** gcc_forest_staging: the current pinned staging slot as a direct buffer of (u32 src, u32 dst) pairs. */
+    static native ByteBuffer staging(long h);
+
+    /** gcc_forest_submit: fold the first nEdges pairs of the staging slot (async); the slot switches. */
+    static native void submit(long h, long nEdges);
+
+    /** gcc_forest_sync. */
+    static native void sync(long h);
+
+    /** gcc_forest_size: getMatches().size() (DisjointSet.java:49-51). */
+    static native long size(long h);
+
+    /** gcc_forest_labels: canonical labels of ids [0, out.length), -1 (GCC_UNSEEN) for unseen ids. */
+    static native void labels(long h, int[] out);
+
+    /** gcc_forest_merge: into := into ∪ from (DisjointSet.merge, :132-136). */
+    static native void merge(long into, long from);
+
+    /** gcc_forest_reset: back to the empty initial value. */
+    static native void reset(long h);
+
+    /** gcc_forest_serialized_size + gcc_forest_serialize: the summary's checkpoint / wire bytes. */
+    static native byte[] serialize(long h);
+
+    /** gcc_forest_deserialize: fold serialized bytes into h. */
+    static native void deserialize(long h, byte[] data);
+}
