@@ -15,12 +15,17 @@ Here the state is one device-resident signed forest (csrc/gelly_bip.hip): per ve
 observable output is canonical: each component keyed by its minimum vertex, every sign relative to that vertex
 (the minimum is `true`). Signs in the reference depend on merge order (the input side is the one reversed), but
 within a component they always agree with ours up to one flip; toString() equals the reference's output whenever
-the reference's minimum vertex carries `true` (as in its own BipartitenessCheckTest). Two observable
-differences, both where the reference is order-dependent or loses information:
-  * a self loop (v, v) only adds v, as in the reference (edgeToCandidate ignores add()'s false, :58-59);
-  * Candidates.merge drops the result of a failed second-level merge (:128-131 call fail() without returning
-    it), so the reference can report success for a graph with an odd cycle closed across two merged summaries;
-    this summary reports the failure.
+the reference's minimum vertex carries `true` (as in its own BipartitenessCheckTest). A self loop (v, v) only adds
+v, as in the reference (edgeToCandidate ignores add()'s false, :58-59). Where the reference's Candidates.merge is
+not a partition join, this summary keeps the intended semantics (bipartite iff no odd cycle) and differs from it:
+  * _merge files the input's vertices under min(inputKey, selfKey) without moving the self component
+    (Candidates.java:176-189): the reference can emit overlapping or split "components";
+  * a failed second-level merge is dropped (:128-131 call fail() without returning it): an odd cycle closed across
+    two merged summaries can be reported as success;
+  * components with identical vertex sets are skipped (:92-95): two partitions over {1,2,3} holding the paths 1-2-3
+    and 1-3-2 form a triangle, which the reference reports as bipartite.
+Every such window of the fixtures is pinned (tests/test_bipartite_oracle.py DIVERGENT, checked on the GPU by
+tests/test_gpu_bipartite.py); DESIGN.md §7.
 """
 from __future__ import annotations
 
