@@ -24,13 +24,15 @@ namespace bk {
 constexpr u32 kSliceBits = 19;                  // ids per slice: 2^19 -> a 64 KiB bitmap slice in LDS
 constexpr u32 kSliceIds = 1u << kSliceBits;
 constexpr u32 kSliceWords = kSliceIds / 32;     // u32 words per slice (16384)
+// P1 geometry (tune.bucket_p1): 0 = 512 threads x 16 edges (8192-edge tiles, 2 blocks per CU), 1 = 1024 x 16
+// (16384-edge tiles, one block per CU: runs twice as long per (tile, bucket))
 constexpr int kP1Block = 512;
 constexpr int kP1Per = 16;                      // edges per thread per tile
-constexpr u32 kP1Tile = kP1Block * kP1Per;      // 8192 edges (64 KiB) per tile
+constexpr u32 kP1Tile = kP1Block * kP1Per;      // the smallest tile (bucket_applies: a batch of >= 2 tiles)
 constexpr int kP2Block = 1024;
 constexpr int kP2Per = 8;                       // edges per thread per round (4 x 16 B)
 constexpr u32 kP2Round = kP2Block * kP2Per;     // 8192 edges per round -> at most 8192 v's per LDS tile
-constexpr u32 kMaxSlicesLds = 512;              // LDS counters: id ranges up to 2^28 (larger: the old path)
+constexpr u32 kMaxSlicesLds = 256;              // LDS per-slice state: id ranges up to 2^27 (larger: the old path)
 constexpr int kP3Block = 1024;
 constexpr u32 kMaxP2Blocks = 1024;
 
@@ -57,13 +59,60 @@ __device__ __forceinline__ u32 lds_bit(const u32* s, u32 x) { return (s[x >> 5] 
 // the sample says; a batch the sample misjudges only overflows (overflow list / inline hooks: still exact).
 constexpr u32 kSample = 1u << 16;
 constexpr u32 kSlack = 1u << 12;
+// Writers reserve space in a bucket / v-list a CHUNK at a time per (block, slice) — one global atomic per chunk,
+// not per tile — and mark the unused tail of their last chunk with UNSEEN at exit (readers skip UNSEEN entries).
+// Each list's capacity therefore carries one chunk per writing block of slack.
+constexpr u32 kChunk = 1024;
 
-__host__ __device__ inline u64 storage_edges(u64 n, u32 ns) { return n + n / 4 + (u64)ns * (kSlack + 64) + 64; }
+__host__ __device__ inline u64 storage_edges(u64 n, u32 ns, u32 blocks) {
+    return n + n / 4 + (u64)ns * (kSlack + 64 + (u64)blocks * kChunk) + 64;
+}
 
-__device__ __forceinline__ u32 est_cap(u32 hits, u64 n, u64 n_smp) {
+__device__ __forceinline__ u32 est_cap(u32 hits, u64 n, u64 n_smp, u32 blocks) {
     const u64 est = (u64)hits * n / (n_smp ? n_smp : 1);
-    const u64 c = ((est + est / 4 + kSlack) + 15) / 16 * 16;  // multiples of 16 entries: 16-B aligned runs
+    const u64 c = ((est + est / 4 + kSlack + (u64)blocks * kChunk) + 15) / 16 * 16;  // 16-entry multiples: aligned
     return (u32)(c < 0xFFFFFFF0ull ? c : 0xFFFFFFF0ull);
+}
+
+// Chunked reservation of this round's run of `c` entries of slice s by the block (one thread per slice): the rest
+// of the block's current chunk [cpos, cend) first, then (if needed) a new chunk of max(kChunk, rest) entries from
+// the list's global cursor, clamped to the capacity. The run's first l1 entries go to p1.., the next l2 to p2..,
+// the remaining c - l1 - l2 (capacity exhausted) overflow. Positions are list-relative.
+struct Runs {
+    u32* cpos;
+    u32* cend;
+    u32* p1;
+    u32* l1;
+    u32* p2;
+    u32* l2;
+};
+
+__device__ __forceinline__ void reserve_run(const Runs& r, u32 s, u32 c, u32* cursor, u32 cap) {
+    const u32 have = r.cend[s] - r.cpos[s];
+    const u32 a = c < have ? c : have;
+    r.p1[s] = r.cpos[s];
+    r.l1[s] = a;
+    r.cpos[s] += a;
+    r.l2[s] = 0;
+    if (c > a) {
+        const u32 need = c - a;
+        const u32 size = ((need > kChunk ? need : kChunk) + 15) / 16 * 16;
+        const u32 g = atomicAdd(cursor, size);
+        const u32 end = g >= cap ? cap : ((u64)g + size > cap ? cap : g + size);
+        const u32 beg = g < cap ? g : cap;
+        const u32 b = need < end - beg ? need : end - beg;
+        r.p2[s] = beg;
+        r.l2[s] = b;
+        r.cpos[s] = beg + b;
+        r.cend[s] = end;
+    }
+}
+
+// The list position of entry i of slice s's run this round, or 0xFFFFFFFF (overflow).
+__device__ __forceinline__ u32 run_pos(const Runs& r, u32 s, u32 i) {
+    if (i < r.l1[s]) return r.p1[s] + i;
+    i -= r.l1[s];
+    return i < r.l2[s] ? r.p2[s] + i : 0xFFFFFFFFu;
 }
 
 // exclusive prefix of cap[0..ns) into base[] (1024 threads, ns <= 1024)
@@ -82,7 +131,7 @@ __device__ __forceinline__ void block_prefix(const u32* cap, u64* base, u32 ns, 
 }
 
 __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
-                                                              Meta* __restrict__ m) {
+                                                              Meta* __restrict__ m, u32 bk_blocks, u32 vl_blocks) {
     __shared__ u32 s_cu[kMaxSlicesLds], s_cv[kMaxSlicesLds];
     __shared__ u64 s_scan[1024];
     for (u32 s = threadIdx.x; s < ns; s += 1024) s_cu[s] = s_cv[s] = 0;
@@ -99,8 +148,8 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     }
     __syncthreads();
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
-        m->bk_cap[s] = est_cap(s_cu[s], n, n_smp);
-        m->vl_cap[s] = est_cap(s_cv[s], n, n_smp);
+        m->bk_cap[s] = est_cap(s_cu[s], n, n_smp, bk_blocks);
+        m->vl_cap[s] = est_cap(s_cv[s], n, n_smp, vl_blocks);
         m->bk_cur[s] = 0;
         m->vl_cur[s] = 0;
     }
@@ -148,22 +197,27 @@ __device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u
 // order and writes every run out contiguously (runs of ~kP1Tile / ns edges). The next tile's loads are in flight
 // meanwhile. Bad ids: skipped + *err. The odd last edge of an odd-length batch and every edge past its bucket's
 // capacity go to the overflow list.
-__global__ __launch_bounds__(kP1Block, 4) void bucket_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
+template <int P1B, int P1P>
+__global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                           Meta* __restrict__ m, u64* __restrict__ bk,
                                                           u64* __restrict__ ovf, u32 ovf_cap, u32* __restrict__ err) {
-    __shared__ u64 s_srt[kP1Tile];
-    __shared__ u32 s_cnt[kMaxSlicesLds], s_start[kMaxSlicesLds], s_g[kMaxSlicesLds], s_cap[kMaxSlicesLds];
+    __shared__ u64 s_srt[(P1B * P1P)];
+    __shared__ u32 s_cnt[kMaxSlicesLds], s_start[kMaxSlicesLds], s_cap[kMaxSlicesLds];
+    __shared__ u32 s_cpos[kMaxSlicesLds], s_cend[kMaxSlicesLds], s_p1[kMaxSlicesLds], s_l1[kMaxSlicesLds],
+        s_p2[kMaxSlicesLds], s_l2[kMaxSlicesLds];
     __shared__ u64 s_base[kMaxSlicesLds];
-    __shared__ u32 s_wsum[kP1Block / 64];
+    __shared__ u32 s_wsum[P1B / 64];
+    const Runs runs{s_cpos, s_cend, s_p1, s_l1, s_p2, s_l2};
     typedef u32 u4 __attribute__((ext_vector_type(4)));
     const u4* body = reinterpret_cast<const u4*>(edges);  // 16-B aligned (bucket_applies checks)
-    for (u32 s = threadIdx.x; s < ns; s += kP1Block) {  // the layout, once per block (not a global load per edge)
+    for (u32 s = threadIdx.x; s < ns; s += P1B) {  // the layout, once per block (not a global load per edge)
         s_cap[s] = m->bk_cap[s];
         s_base[s] = m->bk_base[s];
+        s_cpos[s] = s_cend[s] = 0;  // no chunk yet
     }
     const u64 n2 = n / 2;                                  // whole pairs
-    const u64 ntiles = (n2 * 2 + kP1Tile - 1) / kP1Tile;
-    constexpr int kQ = kP1Per / 2;
+    const u64 ntiles = (n2 * 2 + (P1B * P1P) - 1) / (P1B * P1P);
+    constexpr int kQ = P1P / 2;
     if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) {  // the odd last edge
         u32 a = (u32)edges[n - 1], b = (u32)(edges[n - 1] >> 32);
         if (edge_ok(a, b, cap, err)) {
@@ -175,7 +229,7 @@ __global__ __launch_bounds__(kP1Block, 4) void bucket_kernel(const u64* __restri
     auto load_tile = [&](u64 t, u4 (&q)[kQ]) {
 #pragma unroll
         for (int k = 0; k < kQ; ++k) {
-            const u64 j = t * (kP1Tile / 2) + (u64)k * kP1Block + threadIdx.x;
+            const u64 j = t * ((P1B * P1P) / 2) + (u64)k * P1B + threadIdx.x;
             q[k] = __builtin_nontemporal_load(body + (j < n2 ? j : n2 - 1));  // clamped: countable loads
         }
     };
@@ -183,12 +237,12 @@ __global__ __launch_bounds__(kP1Block, 4) void bucket_kernel(const u64* __restri
     u64 t = blockIdx.x;
     if (t < ntiles) load_tile(t, q);
     for (; t < ntiles; t += gridDim.x) {
-        for (u32 s = threadIdx.x; s < ns; s += kP1Block) s_cnt[s] = 0;
-        u32 ua[kP1Per], va[kP1Per], rk[kP1Per];
-        bool ok[kP1Per];
+        for (u32 s = threadIdx.x; s < ns; s += P1B) s_cnt[s] = 0;
+        u32 ua[P1P], va[P1P], rk[P1P];
+        bool ok[P1P];
 #pragma unroll
         for (int k = 0; k < kQ; ++k) {
-            const u64 j = t * (kP1Tile / 2) + (u64)k * kP1Block + threadIdx.x;
+            const u64 j = t * ((P1B * P1P) / 2) + (u64)k * P1B + threadIdx.x;
             ua[2 * k] = q[k].x;
             va[2 * k] = q[k].y;
             ua[2 * k + 1] = q[k].z;
@@ -198,24 +252,25 @@ __global__ __launch_bounds__(kP1Block, 4) void bucket_kernel(const u64* __restri
         if (t + gridDim.x < ntiles) load_tile(t + gridDim.x, q);  // the next tile streams in meanwhile
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kP1Per; ++k) {
+        for (int k = 0; k < P1P; ++k) {
             if (ok[k]) ok[k] = edge_ok(ua[k], va[k], cap, err);
             if (ok[k]) rk[k] = atomicAdd(&s_cnt[ua[k] >> kSliceBits], 1u);
         }
         __syncthreads();
-        count_scan<kP1Block>(s_cnt, s_start, ns, s_wsum);
-        for (u32 s = threadIdx.x; s < ns; s += kP1Block) s_g[s] = s_cnt[s] ? atomicAdd(&m->bk_cur[s], s_cnt[s]) : 0;
+        count_scan<P1B>(s_cnt, s_start, ns, s_wsum);
+        for (u32 s = threadIdx.x; s < ns; s += P1B)
+            if (s_cnt[s]) reserve_run(runs, s, s_cnt[s], &m->bk_cur[s], s_cap[s]);
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kP1Per; ++k)
+        for (int k = 0; k < P1P; ++k)
             if (ok[k]) s_srt[s_start[ua[k] >> kSliceBits] + rk[k]] = ((u64)va[k] << 32) | ua[k];
         __syncthreads();
         const u32 tot = s_start[ns - 1] + s_cnt[ns - 1];
-        for (u32 x = threadIdx.x; x < tot; x += kP1Block) {
+        for (u32 x = threadIdx.x; x < tot; x += P1B) {
             const u64 e = s_srt[x];
             const u32 s = (u32)e >> kSliceBits;
-            const u64 off = (u64)s_g[s] + (x - s_start[s]);
-            if (off < s_cap[s]) {
+            const u32 off = run_pos(runs, s, x - s_start[s]);
+            if (off != 0xFFFFFFFFu) {
                 bk[s_base[s] + off] = e;
             } else {  // the bucket is full (its estimate was low): the overflow list (folded at the end)
                 const u32 o = atomicAdd(&m->ovf_cur, 1u);
@@ -225,6 +280,9 @@ __global__ __launch_bounds__(kP1Block, 4) void bucket_kernel(const u64* __restri
         }
         __syncthreads();
     }
+    // the unused tails of this block's chunks: UNSEEN edges (P2 skips them)
+    for (u32 s = 0; s < ns; ++s)
+        for (u32 i = s_cpos[s] + threadIdx.x; i < s_cend[s]; i += P1B) bk[s_base[s] + i] = ~0ull;
 }
 
 // Work items of P2 / P3: item i -> (slice i / cps, part i % cps) of a list of `len` entries; the part's range.
@@ -277,9 +335,9 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     u32* s_vt = s_dyn + kSliceWords;                       // kP2Round
     u32* s_cnt2 = s_vt + kP2Round;                         // 2 x kMaxSlicesLds (double-buffered)
     u32* s_start = s_cnt2 + 2 * kMaxSlicesLds;             // kMaxSlicesLds
-    u32* s_g = s_start + kMaxSlicesLds;                    // kMaxSlicesLds
-    u32* s_vcap = s_g + kMaxSlicesLds;                     // kMaxSlicesLds
-    u64* s_vbase = reinterpret_cast<u64*>(s_vcap + kMaxSlicesLds);      // kMaxSlicesLds
+    u32* s_vcap = s_start + kMaxSlicesLds;                 // kMaxSlicesLds
+    u32* s_run = s_vcap + kMaxSlicesLds;                   // 6 x kMaxSlicesLds: the chunk state (Runs)
+    u64* s_vbase = reinterpret_cast<u64*>(s_run + 6 * kMaxSlicesLds);   // kMaxSlicesLds
     u64* ring = s_vbase + kMaxSlicesLds + (threadIdx.x >> 6) * kRing;  // FINAL only
     __shared__ u32 s_item, s_wsum[kP2Block / 64], s_slow;
     typedef u32 u4 __attribute__((ext_vector_type(4)));
@@ -291,9 +349,12 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     u32 cur_slice = 0xFFFFFFFFu;
     u32 rb = 0;  // round parity: the counter buffer in use
     for (u32 s = threadIdx.x; s < 2 * kMaxSlicesLds; s += kP2Block) s_cnt2[s] = 0;
+    const Runs runs{s_run, s_run + kMaxSlicesLds, s_run + 2 * kMaxSlicesLds, s_run + 3 * kMaxSlicesLds,
+                    s_run + 4 * kMaxSlicesLds, s_run + 5 * kMaxSlicesLds};
     for (u32 s = threadIdx.x; s < ns; s += kP2Block) {  // the v-list layout, once per block
         s_vcap[s] = m->vl_cap[s];
         s_vbase[s] = m->vl_base[s];
+        runs.cpos[s] = runs.cend[s] = 0;
     }
     if (threadIdx.x == 0) s_slow = 0;
     const u32 n_items = ns * cps;
@@ -317,58 +378,71 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         const u4* eb = reinterpret_cast<const u4*>(bk + m->bk_base[sl]);  // 16-B aligned (16-edge capacities)
         const u32 sbase = sl << kSliceBits;
         // pairs [lo / 2, ceil(hi / 2)); edges outside [lo, hi) are masked (a part may start or end mid-pair)
-        const u64 plo = lo / 2, phi = (hi + 1) / 2;
+        const u64 plo = lo / 2;
+        const u4* ep = eb + plo;  // this part's pairs, local (32-bit) indices from here on
+        const u32 np = (u32)((hi + 1) / 2 - plo);
+        const bool skip_first = lo & 1, skip_last = hi & 1;  // the part starts / ends in the middle of a pair
         u4 q[kQ];
-        auto load_round = [&](u64 p0) {
+        auto load_round = [&](u32 p0) {
 #pragma unroll
             for (int k = 0; k < kQ; ++k) {
-                const u64 j = p0 + (u64)k * kP2Block + threadIdx.x;
-                q[k] = __builtin_nontemporal_load(eb + (j < phi ? j : phi - 1));  // clamped: countable loads
+                const u32 j = p0 + (u32)k * kP2Block + threadIdx.x;
+                q[k] = __builtin_nontemporal_load(ep + (j < np ? j : np - 1));  // clamped: countable loads
             }
         };
-        load_round(plo);
-        for (u64 p0 = plo; p0 < phi; p0 += kP2Round / 2) {
+        load_round(0);
+        for (u32 p0 = 0; p0 < np; p0 += kP2Round / 2) {
             u32* s_cnt = s_cnt2 + rb * kMaxSlicesLds;
             u32 ua[kP2Per], va[kP2Per], rk[kP2Per];
             bool in[kP2Per];
 #pragma unroll
             for (int k = 0; k < kQ; ++k) {
-                const u64 j = p0 + (u64)k * kP2Block + threadIdx.x;
+                const u32 j = p0 + (u32)k * kP2Block + threadIdx.x;
                 ua[2 * k] = q[k].x;
                 va[2 * k] = q[k].y;
                 ua[2 * k + 1] = q[k].z;
                 va[2 * k + 1] = q[k].w;
-                in[2 * k] = j < phi && 2 * j >= lo && 2 * j < hi;
-                in[2 * k + 1] = j < phi && 2 * j + 1 >= lo && 2 * j + 1 < hi;
+                in[2 * k] = j < np && !(skip_first && j == 0) && ua[2 * k] != 0xFFFFFFFFu;  // UNSEEN: a chunk tail
+                in[2 * k + 1] = j < np && !(skip_last && j == np - 1) && ua[2 * k + 1] != 0xFFFFFFFFu;
             }
-            if (p0 + kP2Round / 2 < phi) load_round(p0 + kP2Round / 2);  // next round in flight
+            if (p0 + kP2Round / 2 < np) load_round(p0 + kP2Round / 2);  // next round in flight
             bool emit[kP2Per];
+            u32 slow_m = 0;  // FINAL: this lane's slow edges (source not in C), bit k
 #pragma unroll
             for (int k = 0; k < kP2Per; ++k) {
                 const u32 iu = in[k] ? lds_bit(s_bits, ua[k] - sbase) : 0u;
                 emit[k] = in[k] && iu;
                 if (emit[k]) rk[k] = atomicAdd(&s_cnt[va[k] >> kSliceBits], 1u);
-                if constexpr (FINAL) {  // a slow edge: into this block's region of the slow list (wave-aggregated)
-                    const bool sl_e = in[k] && !iu;
-                    const unsigned long long bm = __ballot(sl_e);
-                    bool spill = false;
-                    if (bm) {
-                        u32 base = 0;
-                        if (lane == 0) base = atomicAdd(&s_slow, (u32)__popcll(bm));
-                        base = __shfl(base, 0, 64);
-                        const u32 pos = base + (u32)__popcll(bm & ((1ull << lane) - 1ull));
-                        if (sl_e) {
-                            if (pos < slow_cap) my_slow[pos] = ((u64)va[k] << 32) | ua[k];
-                            else spill = true;
-                        }
+                slow_m |= (u32)(in[k] && !iu) << k;
+            }
+            if constexpr (FINAL) {  // the slow edges: into this block's region of the slow list, one LDS add per wave
+                const u32 ns_l = (u32)__popc(slow_m);
+                u32 incl = ns_l;
+                for (int o = 1; o < 64; o <<= 1) {
+                    const u32 y = __shfl_up(incl, o, 64);
+                    if (lane >= (u32)o) incl += y;
+                }
+                u32 base = 0;
+                if (lane == 63 && incl) base = atomicAdd(&s_slow, incl);
+                base = __shfl(base, 63, 64);
+                u32 pos = base + incl - ns_l, spill_m = 0;
+#pragma unroll
+                for (int k = 0; k < kP2Per; ++k)
+                    if ((slow_m >> k) & 1u) {
+                        if (pos < slow_cap) my_slow[pos] = ((u64)va[k] << 32) | ua[k];
+                        else spill_m |= 1u << k;
+                        ++pos;
                     }
-                    ring_push(spill, ua[k], va[k], ring, wq, wd, parent, drain_at, 0xFFFFFFFFu);  // past the region
+                if (__ballot(spill_m != 0)) {  // past the region (never at the default sizes): united right here
+#pragma unroll
+                    for (int k = 0; k < kP2Per; ++k)
+                        ring_push((spill_m >> k) & 1u, ua[k], va[k], ring, wq, wd, parent, drain_at, 0xFFFFFFFFu);
                 }
             }
             __syncthreads();  // (1) counts of this round complete
             count_scan<kP2Block>(s_cnt, s_start, ns, s_wsum);
             for (u32 s = threadIdx.x; s < ns; s += kP2Block) {
-                s_g[s] = s_cnt[s] ? atomicAdd(&m->vl_cur[s], s_cnt[s]) : 0;
+                if (s_cnt[s]) reserve_run(runs, s, s_cnt[s], &m->vl_cur[s], s_vcap[s]);
                 s_cnt2[(rb ^ 1) * kMaxSlicesLds + s] = 0;  // the next round's buffer
             }
             __syncthreads();  // (2) starts + reservations
@@ -380,13 +454,17 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             for (u32 x = threadIdx.x; x < tot; x += kP2Block) {
                 const u32 v = s_vt[x];
                 const u32 s = v >> kSliceBits;
-                const u64 off = (u64)s_g[s] + (x - s_start[s]);
-                if (off < s_vcap[s]) vl[s_vbase[s] + off] = v;
+                const u32 off = run_pos(runs, s, x - s_start[s]);
+                if (off != 0xFFFFFFFFu) vl[s_vbase[s] + off] = v;
                 else if (FINAL) hook_g(parent, g, v);  // the v-list is full: (u in C, v) = union(g, v) now
             }
             rb ^= 1;  // the write-out above is done before anyone passes the next round's barrier (1)
         }
     }
+    __syncthreads();
+    // the unused tails of this block's chunks: UNSEEN (P3 skips them)
+    for (u32 s = 0; s < ns; ++s)
+        for (u32 i = runs.cpos[s] + threadIdx.x; i < runs.cend[s]; i += kP2Block) vl[s_vbase[s] + i] = 0xFFFFFFFFu;
     if constexpr (FINAL) {  // the rest of this wave's ring; the block's slow count
         for (; wd < wq; wd += 64) {
             if (lane < wq - wd) {
@@ -424,6 +502,7 @@ __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ 
         }
     };
     auto visit = [&](u32 v, u32 sbase) {
+        if (v == 0xFFFFFFFFu) return;  // a chunk tail (P2)
         const u32 x = v - sbase, msk = 1u << (x & 31);
         if (s_bits[x >> 5] & msk) return;                  // already in C (or taken by this block)
         if (atomicOr(&s_bits[x >> 5], msk) & msk) return;  // another lane of the block took it

@@ -65,7 +65,9 @@ int gcc_set_err(int code, const char* fmt, ...) {
 // ------------------------------------------------------------------------------------------------
 using gcc::Count;
 using gcc::NoCount;
-typedef gcc::UnionFind<gcc::LoadPlain, true> UF;
+using gcc::UF;
+using gcc::UFRead;
+using gcc::unite_entry;
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 typedef uint8_t u8;
 
@@ -145,18 +147,9 @@ constexpr u32 kRing = 128;  // u64 entries per wave (1 KiB): pending stays < 64 
 
 // One drain round: the wave unites up to 64 ring entries, one per lane. Out of line: it runs rarely, and
 // inlined at each of the hot loop's 8 push sites it multiplied the loop body ~8x (I-cache, registers).
-// The union of one ring entry. An entry (g, x) with x > g (an edge from the tracked component to an id outside
-// it) takes the hook of filter_round: ONE atomicMin(parent[x], g); only if x already hung under some other id
-// p (old not in {UNSEEN, x, g}) is the link to p restored by union(g, p). Anything else: the full union.
-__device__ __forceinline__ void unite_entry(u32* parent, u32 a, u32 b, u32 g) {
-    NoCount c;
-    if (a == g && b > g) {
-        const u32 old = atomicMin(&parent[b], g);
-        if (old != UNSEEN && old != b && old != g) UF::unite(parent, g, old, c);
-    } else {
-        UF::unite(parent, a, b, c);
-    }
-}
+// The union of one ring entry (uf_device.h unite_entry): an entry (g, x) with x > g (an edge from the tracked
+// component to an id outside it) takes the hook of filter_round: ONE atomicMin(parent[x], g); only if x already hung
+// under some other id p (old not in {UNSEEN, x, g}) is the link to p restored by union(g, p). Else the full union.
 
 __device__ __attribute__((noinline)) void ring_drain(const u64* ring, u32 wd, u32 pending, u32* parent, u32 g) {
     const u32 lane = threadIdx.x & 63;
@@ -210,7 +203,7 @@ struct HookCarry {
     __device__ __forceinline__ void settle(u32 g, u64* ring, u32& wq, u32& wd, u32* parent, u32 drain_at) {
 #pragma unroll
         for (int k = 0; k < N; ++k) {
-            const bool again = hook[k] && old[k] != GCC_UNSEEN && old[k] != other[k] && old[k] != g;
+            const bool again = hook[k] && gcc::hook_needs_union(old[k], other[k], g);
             ring_push(again, g, again ? old[k] : 0u, ring, wq, wd, parent, drain_at, g);
         }
     }
@@ -236,7 +229,7 @@ __device__ __forceinline__ void filter_round(const bool* valid, const u32* a, co
         slow[k] = valid[k] && !(ia & ib) && !cur.hook[k];
         pa[k] = ia ? g : a[k];
         pb[k] = ib ? g : b[k];
-        if (cur.hook[k]) cur.old[k] = atomicMin(&parent[cur.other[k]], g);
+        if (cur.hook[k]) cur.old[k] = gcc::hook_min(parent, cur.other[k], g);
     }
     carry.settle(g, ring, wq, wd, parent, drain_at);  // the previous round's hooks (their atomics have returned)
 #pragma unroll
@@ -410,13 +403,9 @@ __global__ __launch_bounds__(kBlock) void merge_labels_kernel(u32* __restrict__ 
 // needs to stay a valid forest (every store is an ancestor, roots never move: no hook is in flight).
 // Algorithmic traffic: 4 B read + 4 B write per id (chain reads hit L2).
 __global__ __launch_bounds__(kBlock) void compress_kernel(u32* __restrict__ parent, u32* __restrict__ labels, u32 n) {
-    NoCount c;
     const u64 stride = (u64)gridDim.x * kBlock;
-    for (u64 vv = (u64)blockIdx.x * kBlock + threadIdx.x; vv < n; vv += stride) {
-        const u32 v = (u32)vv;
-        const u32 p = parent[v];
-        labels[v] = (p >= v) ? p : UF::find_from(parent, v, p, c);  // root / UNSEEN: itself
-    }
+    for (u64 vv = (u64)blockIdx.x * kBlock + threadIdx.x; vv < n; vv += stride)
+        labels[vv] = gcc::compress_label(parent, (u32)vv);  // root / UNSEEN: itself
 }
 
 // Majority vote (Boyer-Moore in its associative pair form) over the labels of 4096 pseudo-random seen ids:
@@ -533,15 +522,7 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
 // bloom in LDS; a lane reads 4 consecutive ids (16 B) and a wave covers 256 ids = 4 bitmap words of the
 // tracked component (as compress_bits_kernel). The block also clears its share of the other bloom buffer.
 constexpr int kIncBlock = 1024;
-typedef gcc::UnionFind<gcc::LoadPlain, false> UFRead;
-
-__device__ __forceinline__ u32 inc_label(const u32* parent, const u32* s_bloom, u32 v, u32 p) {
-    if (p >= v) return p;  // root (p == v) or UNSEEN
-    const u32 s = gcc::bloom_slot(p);
-    if (!((s_bloom[s >> 5] >> (s & 31)) & 1u)) return p;
-    NoCount c;
-    return UFRead::find_from(const_cast<u32*>(parent), v, p, c);
-}
+using gcc::inc_label;  // uf_device.h: shared with the host replay
 
 // INPLACE: labels == parent. parent[] is already canonical except where a marked parent needs the find, so only
 // those slots are written (with the root; each slot by its own lane only). That is race-free: the finds are
@@ -1045,7 +1026,6 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict
     __shared__ u32 s_g[kMaxPeers];
     __shared__ u32 s_w[kMaxPeers];
     msg_peers(msgs, stride, count, skip, n, true, witness, s_g, s_w);
-    NoCount c;
     const u32 lane = threadIdx.x & 63;
     const u32 R = *tracked;
     const u64 nw = ((u64)n + 63) / 64;
@@ -1060,10 +1040,7 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict
         if (!m) continue;
         const u64 todo = m & ~mine[w];
         const u32 v = (u32)(w * 64 + lane);
-        if (((todo >> lane) & 1ull) && v != R) {
-            if (v > R && parent[v] == UNSEEN) parent[v] = R;  // new id: seen and hung under R in one store
-            else UF::unite(parent, v, R, c);
-        }
+        if (((todo >> lane) & 1ull) && v != R) gcc::absorb_join(parent, v, R);  // a new id: one plain store
     }
 }
 
@@ -1115,7 +1092,7 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
 #include "bucket_fold.h"
 
 static constexpr size_t slice_filter_lds() {  // bucket_fold.h slice_filter_kernel's dynamic LDS
-    return (bk::kSliceWords + bk::kP2Round + 5 * bk::kMaxSlicesLds) * sizeof(u32) + bk::kMaxSlicesLds * sizeof(u64) +
+    return (bk::kSliceWords + bk::kP2Round + 10 * bk::kMaxSlicesLds) * sizeof(u32) + bk::kMaxSlicesLds * sizeof(u64) +
            (bk::kP2Block / 64) * kRing * sizeof(u64);
 }
 
@@ -1211,6 +1188,7 @@ struct FoldTune {
     int bucket_levels = 3;
     double bucket_sample = 0.25;
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
+    int bucket_p1 = 0;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -1642,10 +1620,11 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (rc) return rc;
     const u32 ns = bucket_slices(h);
     if (!h->d_meta) HIP_TRY(hipMalloc((void**)&h->d_meta, sizeof(bk::Meta)));
-    if ((rc = grow(h->d_bk, h->bk_cap_edges, bk::storage_edges(n, ns)))) return rc;
-    if ((rc = grow(h->d_ovf, h->ovf_cap, n / 8 + 65536))) return rc;
-    if ((rc = grow(h->d_vl, h->vl_cap, bk::storage_edges(n, ns)))) return rc;
+    const u32 p1_blocks = 2 * (u32)h->n_cu;  // (bucket_p1 = 1 runs n_cu blocks: fewer writers, same slack bound)
     const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
+    if ((rc = grow(h->d_bk, h->bk_cap_edges, bk::storage_edges(n, ns, p1_blocks)))) return rc;
+    if ((rc = grow(h->d_ovf, h->ovf_cap, n / 8 + 65536))) return rc;
+    if ((rc = grow(h->d_vl, h->vl_cap, bk::storage_edges(n, ns, p2_blocks)))) return rc;
     const u32 slow_cap = (u32)std::min<u64>(0x7FFFFFFFull, std::max<u64>(4096, n / p2_blocks / 8));
     if ((rc = grow(h->d_slow, h->slow_cap_total, (u64)p2_blocks * slow_cap))) return rc;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
@@ -1662,9 +1641,13 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const size_t f_lds = slice_filter_lds(), h_lds = bk::kSliceWords * sizeof(u32);
     const size_t vl_cur_off = offsetof(bk::Meta, vl_cur);
     u32 slot = 0;
-    rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta);
+    rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta,
+                  p1_blocks, p2_blocks);
     if (!rc)
-        rc = launch_k(h, "bucket", n, bk::bucket_kernel, dim3(2 * h->n_cu), dim3(bk::kP1Block), 0, edges, n, ns, h->cap,
+        rc = t.bucket_p1 == 1
+                 ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16>, dim3(h->n_cu), dim3(1024), 0, edges, n, ns, h->cap,
+                            h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err)
+                 : launch_k(h, "bucket", n, bk::bucket_kernel<512, 16>, dim3(p1_blocks), dim3(512), 0, edges, n, ns, h->cap,
                       h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err);
     if (rc) return rc;
     // seeding: C := {hub}, then levels over the sample
@@ -2649,6 +2632,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "inc_min_ids") t.inc_min_ids = (u64)value;
     else if (k == "inc_div") t.inc_div = std::max<u64>(1, (u64)value);
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
+    else if (k == "bucket_p1") t.bucket_p1 = (int)value == 1 ? 1 : 0;
     else if (k == "bucket") t.bucket = value != 0;
     else if (k == "bucket_min_batch") t.bucket_min_batch = (u64)value;
     else if (k == "bucket_min_ids") t.bucket_min_ids = (u64)value;

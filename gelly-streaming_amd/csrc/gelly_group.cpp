@@ -282,7 +282,7 @@ int gcc_group_merge(gcc_forest** hs, int n, gcc_comm** comms) {
         // one grouped launch of every rank's collective (a single thread drives all of them)
         ABI_TRY(rccl_ready());
         u64 cap = std::max<u64>(1024, V[0] / 64);
-        for (int round = 0;; ++round) {
+        while (true) {
             const u64 size = round16(gcc_msg_bytes(V[0], cap));
             const bool labels = size >= 4ull * V[0];
             for (int i = 0; i < n; ++i) {

@@ -1,12 +1,19 @@
-// uf_device.h — device union-find primitives over a u32 parent[] forest (min-id hooking), shared by the
-// product kernels (gelly_cc.hip) and the measurement probes (tools/probe_fold.hip).
+// uf_device.h — union-find primitives over a u32 parent[] forest (min-id hooking), shared by the product kernels
+// (gelly_cc.hip, bucket_fold.h), the measurement probes (tools/probe_fold.hip) and the HOST replay harness
+// (tests/cpp/test_uf_replay.cpp), which runs these exact functions on host threads with relaxed atomics and
+// injected stale loads. Compiled by hipcc (device + host) and by g++ (host only: no HIP headers).
 //
 // Forest encoding: parent[v] == UNSEEN -> v not in the key set; parent[v] == v -> root; parent[v] < v otherwise.
 // Reference semantics restated: DisjointSet.makeSet/find/union (…/summaries/DisjointSet.java:58-123); see
 // gelly_cc.hip's header for the memory-model argument (stale reads are historically valid, CAS returns fresh).
 #pragma once
-#include <hip/hip_runtime.h>
 #include <stdint.h>
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define UF_HD __host__ __device__ __forceinline__
+#else
+#define UF_HD inline
+#endif
 
 #define GCC_UNSEEN_DEV 0xFFFFFFFFu
 
@@ -15,10 +22,76 @@ namespace gcc {
 typedef uint32_t u32;
 typedef uint64_t u64;
 
-// load policies for parent[] reads
-struct LoadPlain {  // global_load: L1 -> L2
-    static __device__ __forceinline__ u32 ld(const u32* p) { return *p; }
+// ---- word-level memory operations: device intrinsics, or (host replay) relaxed __atomic builtins ----------------
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host replay only (tests/cpp/test_uf_replay.cpp): a scheduling point before every memory operation (a controlled
+// scheduler interleaves the threads there), the value a plain load returns (a stale but historically valid one may
+// be injected), and a note of every value a store or atomic wrote (the history loads may be answered from).
+struct ReplayHooks {
+    virtual void before(const u32* p) = 0;
+    virtual u32 load(const u32* p, u32 fresh) = 0;
+    virtual void wrote(const u32* p, u32 v) = 0;
 };
+inline ReplayHooks* replay = nullptr;  // null: plain relaxed atomics (product host code never sets it)
+#define UF_REPLAY_BEFORE(p) \
+    if (replay) replay->before(p)
+#define UF_REPLAY_WROTE(p, v) \
+    if (replay) replay->wrote(p, v)
+#endif
+
+UF_HD u32 ld(const u32* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *p;  // global_load: L1 -> L2 (may be stale inside a kernel: historically valid)
+#else
+    UF_REPLAY_BEFORE(p);
+    const u32 fresh = __atomic_load_n(p, __ATOMIC_RELAXED);
+    return replay ? replay->load(p, fresh) : fresh;
+#endif
+}
+UF_HD void st(u32* p, u32 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *p = v;  // a plain (vector) store
+#else
+    UF_REPLAY_BEFORE(p);
+    __atomic_store_n(p, v, __ATOMIC_RELAXED);
+    UF_REPLAY_WROTE(p, v);
+#endif
+}
+UF_HD u32 cas(u32* p, u32 cmp, u32 val) {  // returns the old value (fresh: executed at the memory side)
+#if defined(__HIP_DEVICE_COMPILE__)
+    return atomicCAS(p, cmp, val);
+#else
+    UF_REPLAY_BEFORE(p);
+    if (__atomic_compare_exchange_n(p, &cmp, val, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) UF_REPLAY_WROTE(p, val);
+    return cmp;
+#endif
+}
+UF_HD u32 amin(u32* p, u32 v) {  // returns the old value
+#if defined(__HIP_DEVICE_COMPILE__)
+    return atomicMin(p, v);
+#else
+    UF_REPLAY_BEFORE(p);
+    u32 old = __atomic_load_n(p, __ATOMIC_RELAXED);
+    while (old > v && !__atomic_compare_exchange_n(p, &old, v, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+    }
+    if (old > v) UF_REPLAY_WROTE(p, v);
+    return old;
+#endif
+}
+UF_HD void aor(u32* p, u32 m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicOr(p, m);
+#else
+    UF_REPLAY_BEFORE(p);
+    __atomic_fetch_or(p, m, __ATOMIC_RELAXED);
+#endif
+}
+
+// load policies for parent[] reads
+struct LoadPlain {  // global_load: L1 -> L2 (host replay: relaxed load + optional stale injection)
+    static UF_HD u32 ld(const u32* p) { return gcc::ld(p); }
+};
+#if defined(__HIPCC__)
 struct LoadAgent {  // relaxed agent-scope atomic load (sc1): bypasses the CU's L1, served by the XCD's L2
     static __device__ __forceinline__ u32 ld(const u32* p) {
         return __hip_atomic_load(const_cast<u32*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -29,20 +102,21 @@ struct LoadSystem {  // relaxed system-scope atomic load (sc0 sc1)
         return __hip_atomic_load(const_cast<u32*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 };
+#endif
 
 // optional per-thread event counters (probe builds only)
 struct NoCount {
-    __device__ __forceinline__ void cas() {}
-    __device__ __forceinline__ void cas_fail() {}
-    __device__ __forceinline__ void step() {}
-    __device__ __forceinline__ void store() {}
+    UF_HD void cas() {}
+    UF_HD void cas_fail() {}
+    UF_HD void step() {}
+    UF_HD void store() {}
 };
 struct Count {
     u32 n_cas = 0, n_fail = 0, n_step = 0, n_store = 0;
-    __device__ __forceinline__ void cas() { ++n_cas; }
-    __device__ __forceinline__ void cas_fail() { ++n_fail; }
-    __device__ __forceinline__ void step() { ++n_step; }
-    __device__ __forceinline__ void store() { ++n_store; }
+    UF_HD void cas() { ++n_cas; }
+    UF_HD void cas_fail() { ++n_fail; }
+    UF_HD void step() { ++n_step; }
+    UF_HD void store() { ++n_store; }
 };
 
 // Mutation recorder for the incremental compress (gelly_cc.hip compress_inc_kernel). Between two compresses,
@@ -53,26 +127,26 @@ struct Count {
 // p that is some id's parent is still a root: that id's label is p, no find needed. Ids that leave UNSEEN need
 // no mark: one hung straight under a root never becomes a parent value, one made a root is marked if hooked.
 constexpr u32 kBloomBits = 1u << 20;  // 128 KiB: one CU's LDS copy in the incremental compress
-__host__ __device__ __forceinline__ u32 bloom_slot(u32 x) { return (x * 0x9E3779B1u) >> 12; }
+UF_HD u32 bloom_slot(u32 x) { return (x * 0x9E3779B1u) >> 12; }
 struct NoRec {
-    __device__ __forceinline__ void mark(u32) const {}
+    UF_HD void mark(u32) const {}
 };
 struct BloomRec {
     u32* bloom;
-    __device__ __forceinline__ void mark(u32 x) const {
+    UF_HD void mark(u32 x) const {
         const u32 s = bloom_slot(x);
-        atomicOr(&bloom[s >> 5], 1u << (s & 31));
+        aor(&bloom[s >> 5], 1u << (s & 31));
     }
 };
 
 template <class L, bool SPLIT, class C = NoCount>
 struct UnionFind {
     // makeSet-on-first-sight (DisjointSet.union :99-104): an observed parent of v that is not UNSEEN
-    static __device__ __forceinline__ u32 seen_parent(u32* parent, u32 v, C& c) {
+    static UF_HD u32 seen_parent(u32* parent, u32 v, C& c) {
         u32 p = L::ld(&parent[v]);
         if (p == GCC_UNSEEN_DEV) {
             c.cas();
-            const u32 old = atomicCAS(&parent[v], GCC_UNSEEN_DEV, v);
+            const u32 old = gcc::cas(&parent[v], GCC_UNSEEN_DEV, v);
             p = (old == GCC_UNSEEN_DEV) ? v : old;
         }
         return p;
@@ -80,7 +154,7 @@ struct UnionFind {
 
     // find (DisjointSet.find :71-85) from x with observed parent p; optional path splitting (plain stores of
     // grandparents into non-root slots). p >= x means x is a root (or p is a stale UNSEEN).
-    static __device__ __forceinline__ u32 find_from(u32* parent, u32 x, u32 p, C& c) {
+    static UF_HD u32 find_from(u32* parent, u32 x, u32 p, C& c) {
         if (p >= x) return x;
         u32 prev = x, cur = p;
         while (true) {
@@ -88,7 +162,7 @@ struct UnionFind {
             const u32 next = L::ld(&parent[cur]);
             if (next >= cur) break;
             if (SPLIT) {
-                parent[prev] = next;
+                gcc::st(&parent[prev], next);
                 c.store();
             }
             prev = cur;
@@ -97,16 +171,16 @@ struct UnionFind {
         return cur;
     }
 
-    // union (DisjointSet.union :97-123), min-id hooking with atomicCAS on the larger root.
+    // union (DisjointSet.union :97-123), min-id hooking with a CAS on the larger root.
     // An unseen endpoint v joining a component whose root r < v is made seen AND hung under r by ONE CAS
     // (UNSEEN -> r): the common case of a stream (a new vertex attaching to an existing component).
     template <class R = NoRec>
-    static __device__ __forceinline__ void unite(u32* parent, u32 u, u32 v, C& c, const R& rec = R()) {
+    static UF_HD void unite(u32* parent, u32 u, u32 v, C& c, const R& rec = R()) {
         u32 pu = L::ld(&parent[u]);
         if (u == v) {  // self loop: makeSet only
             if (pu == GCC_UNSEEN_DEV) {
                 c.cas();
-                atomicCAS(&parent[u], GCC_UNSEEN_DEV, u);
+                gcc::cas(&parent[u], GCC_UNSEEN_DEV, u);
             }
             return;
         }
@@ -119,7 +193,7 @@ struct UnionFind {
         if (pu == GCC_UNSEEN_DEV) {  // both unseen: make the smaller one seen (a root unless raced)
             const u32 lo = u < v ? u : v, hi = u < v ? v : u;
             c.cas();
-            const u32 o = atomicCAS(&parent[lo], GCC_UNSEEN_DEV, lo);
+            const u32 o = gcc::cas(&parent[lo], GCC_UNSEEN_DEV, lo);
             u = lo;
             pu = (o == GCC_UNSEEN_DEV) ? lo : o;
             v = hi;
@@ -128,11 +202,11 @@ struct UnionFind {
         if (pv == GCC_UNSEEN_DEV) {
             c.cas();
             if (ru < v) {
-                const u32 o = atomicCAS(&parent[v], GCC_UNSEEN_DEV, ru);
+                const u32 o = gcc::cas(&parent[v], GCC_UNSEEN_DEV, ru);
                 if (o == GCC_UNSEEN_DEV) return;  // v seen and hooked under ru in one step
                 pv = o;
             } else {
-                const u32 o = atomicCAS(&parent[v], GCC_UNSEEN_DEV, v);
+                const u32 o = gcc::cas(&parent[v], GCC_UNSEEN_DEV, v);
                 pv = (o == GCC_UNSEEN_DEV) ? v : o;
             }
         }
@@ -141,14 +215,14 @@ struct UnionFind {
             const u32 lo = ru < rv ? ru : rv;
             const u32 hi = ru < rv ? rv : ru;
             c.cas();
-            u32 old = atomicCAS(&parent[hi], hi, lo);
+            u32 old = gcc::cas(&parent[hi], hi, lo);
             if (old == hi) {
                 rec.mark(hi);
                 return;
             }
             c.cas_fail();
             if (old == GCC_UNSEEN_DEV) {  // unreachable for seen roots; keeps the loop finite regardless
-                old = atomicCAS(&parent[hi], GCC_UNSEEN_DEV, lo);
+                old = gcc::cas(&parent[hi], GCC_UNSEEN_DEV, lo);
                 if (old == GCC_UNSEEN_DEV) {
                     rec.mark(hi);
                     return;
@@ -159,5 +233,53 @@ struct UnionFind {
         }
     }
 };
+
+typedef UnionFind<LoadPlain, true> UF;       // the fold's union (path splitting)
+typedef UnionFind<LoadPlain, false> UFRead;  // read-only finds (compress)
+
+// ---- the per-id and per-edge steps of the other kernels, shared with the host replay ------------------------
+
+// The filtered fold's direct hook of an edge (g, b) with g in the tracked component and b > g outside it
+// (gelly_cc.hip filter_round), in its two halves: the atomicMin, issued for a whole round first, and its check
+// ("settle") one round later: old = UNSEEN (b was new), b (b was a root) or g: b now hangs under g, done;
+// otherwise b left the tree of old (or already hung lower), and union(g, old) restores the connection.
+UF_HD u32 hook_min(u32* parent, u32 b, u32 g) { return amin(&parent[b], g); }
+UF_HD bool hook_needs_union(u32 old, u32 b, u32 g) { return old != GCC_UNSEEN_DEV && old != b && old != g; }
+
+// A ring entry of the filtered fold (gelly_cc.hip unite_entry): (g, x) with x > g takes the hook form in one step.
+UF_HD void unite_entry(u32* parent, u32 a, u32 b, u32 g) {
+    NoCount c;
+    if (a == g && b > g) {
+        const u32 old = hook_min(parent, b, g);
+        if (hook_needs_union(old, b, g)) UF::unite(parent, g, old, c);
+    } else {
+        UF::unite(parent, a, b, c);
+    }
+}
+
+// msg_absorb_bits_kernel: an id x of a peer's giant, outside this forest's tracked component T (root R), joins R.
+// A new id above R by a PLAIN store — in that kernel x has no other writer — anything else by the union.
+UF_HD void absorb_join(u32* parent, u32 x, u32 R) {
+    NoCount c;
+    if (x > R && ld(&parent[x]) == GCC_UNSEEN_DEV) st(&parent[x], R);
+    else UF::unite(parent, x, R, c);
+}
+
+// compress_kernel's per-id step (out of place): labels[v] = root(v), UNSEEN stays UNSEEN.
+UF_HD u32 compress_label(u32* parent, u32 v) {
+    NoCount c;
+    const u32 p = ld(&parent[v]);
+    return (p >= v) ? p : UF::find_from(parent, v, p, c);
+}
+
+// compress_inc_kernel's per-id step: after a compress, parent[] IS the label array; an unmarked parent p is
+// still a root (BloomRec), so labels[v] = p without a find; a marked one takes a read-only find.
+UF_HD u32 inc_label(const u32* parent, const u32* bloom, u32 v, u32 p) {
+    if (p >= v) return p;  // root (p == v) or UNSEEN
+    const u32 s = bloom_slot(p);
+    if (!((bloom[s >> 5] >> (s & 31)) & 1u)) return p;
+    NoCount c;
+    return UFRead::find_from(const_cast<u32*>(parent), v, p, c);
+}
 
 }  // namespace gcc

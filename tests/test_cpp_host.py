@@ -17,7 +17,8 @@ def test_cpp_mirror_builds():
 
 @pytest.mark.gpu
 def test_cpp_mirror_reference_tests():
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
+    # rebuilt here (-B): a binary that arrived with the snapshot may not be executable on the GPU box
+    subprocess.run(["make", "-s", "-B", "-C", os.path.join(ROOT, "tests", "cpp"), "build/test_host_mirror"], check=True)
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr

@@ -528,6 +528,7 @@ KNOB_CASES = {
     "bucket_levels": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_levels": 1},
     "bucket_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_sample": 1.0},
     "pin_chunk": {"pin_chunk": 4096},
+    "bucket_p1": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 1},
 }
 
 
@@ -561,6 +562,7 @@ def test_every_tuning_knob_is_bit_exact(torch_cuda):
         with pytest.raises(GellyCCError):
             ds.tune(no_such_knob=1)
     for key, knobs in KNOB_CASES.items():
+        print("knob case", key, flush=True)  # names the case in the report if a launch faults asynchronously
         with DisjointSet(V) as ds:
             ds.tune(**knobs)
             for w in range(len(starts) - 1):
