@@ -1186,9 +1186,9 @@ struct FoldTune {
     u64 bucket_min_batch = 1ull << 25;
     u64 bucket_min_ids = (u64)kLdsBitmapMaxWords * 64 + 1;
     int bucket_levels = 3;
-    double bucket_sample = 0.25;
+    double bucket_sample = 0.15;  // profiles/r2_sweep_c4_p1.log: 0.25 -> 0.15 = 12.74 -> 12.22 ms on C4
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
-    int bucket_p1 = 0;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16
+    int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 

@@ -528,7 +528,7 @@ KNOB_CASES = {
     "bucket_levels": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_levels": 1},
     "bucket_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_sample": 1.0},
     "pin_chunk": {"pin_chunk": 4096},
-    "bucket_p1": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 1},
+    "bucket_p1": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 0},
 }
 
 
