@@ -41,8 +41,10 @@ KERNEL_BYTES = {
     "seed_pack_kernel": (5.125, "id"),      # flag byte read + parent write + 1 bitmap bit (the init variant)
     "seed_hub_kernel": (1.125, "id"),       # flag byte + bitmap bit cleared
     "bucket_kernel": (16, "edge"),          # read the edge + write it into its u-slice bucket
-    "slice_filter_kernel": (12, "edge"),    # read the bucketed edge + write v of u-in-giant edges (4 B)
-    "slice_hook_kernel": (4, "edge"),       # read the v list
+    "slice_filter_kernel<true>": (12, "edge"),   # FINAL P2: read the bucketed edge + write v of u-in-C edges (4 B)
+    "slice_filter_kernel<false>": (12, "edge"),  # a seeding level's P2 over the bucket samples
+    "slice_hook_kernel<true>": (4, "edge"),      # FINAL P3: read the v-lists (units: the batch's edges)
+    "slice_hook_kernel<false>": (4, "edge"),     # a seeding level's P3
     "bucket_init_kernel": (4.125, "id"),    # parent write + 1 bitmap bit
 }
 C2_BATCHES = 4  # rotating C2 batches (tests/golden/stream_digests.json c2_rmat20@k)
@@ -170,9 +172,11 @@ def kernel_stats(log, V, inst_steps):
                  "seed_init": "seed_pack_kernel", "refresh": "compress_bits_kernel", "compress": "compress_bits_kernel",
                  "refresh_bits": "compress_bits_kernel", "compress_inc": "compress_inc_kernel",
                  "refresh_inc": "compress_inc_kernel", "vote": "giant_vote_kernel", "bucket": "bucket_kernel",
-                 "bucket_hist": "bucket_hist_kernel", "slice_filter": "slice_filter_kernel",
-                 "seed_filter": "slice_filter_kernel", "slice_hook": "slice_hook_kernel",
-                 "seed_hook": "slice_hook_kernel", "bucket_init": "bucket_init_kernel", "overflow": "fold_filtered_kernel"}
+                 "bucket_hist": "bucket_hist_kernel", "slice_filter": "slice_filter_kernel<true>",
+                 "seed_filter": "slice_filter_kernel<false>", "slice_hook": "slice_hook_kernel<true>",
+                 "seed_hook": "slice_hook_kernel<false>", "bucket_hook": "bucket_hook_kernel",
+                 "bucket_slow": "bucket_slow_kernel", "bucket_rest": "bucket_rest_kernel",
+                 "bucket_layout": "bucket_layout_kernel", "bucket_hub": "bucket_hub_kernel", "bucket_init": "bucket_init_kernel", "overflow": "fold_filtered_kernel"}
     phases, kernels, spans = {}, {}, []
     for name, ms, n in log:
         if name in ("begin", "slow_edges"):
