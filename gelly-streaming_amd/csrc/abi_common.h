@@ -12,13 +12,15 @@
 int gcc_set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 // the device exists and is a gfx950 (this library carries gfx950 code only)
 int gcc_check_device(int device);
+// after an asynchronous kernel fault: " [last kernel started: <name>]" from the kernel-start trace (gelly_cc.hip)
+const char* gcc_fault_note(hipError_t e);
 
 #define HIP_TRY(expr)                                                                                      \
     do {                                                                                                   \
         hipError_t e_ = (expr);                                                                            \
         if (e_ != hipSuccess) {                                                                            \
-            return gcc_set_err(e_ == hipErrorOutOfMemory ? GCC_E_OOM : GCC_E_HIP, "%s failed: %s (%s:%d)", \
-                               #expr, hipGetErrorString(e_), __FILE__, __LINE__);                          \
+            return gcc_set_err(e_ == hipErrorOutOfMemory ? GCC_E_OOM : GCC_E_HIP, "%s failed: %s (%s:%d)%s", \
+                               #expr, hipGetErrorString(e_), __FILE__, __LINE__, gcc_fault_note(e_));       \
         }                                                                                                  \
     } while (0)
 

@@ -54,6 +54,13 @@ struct Meta {
 
 __device__ __forceinline__ u32 lds_bit(const u32* s, u32 x) { return (s[x >> 5] >> (x & 31)) & 1u; }
 
+// Internal consistency checks: every entry a kernel takes from an internal list (buckets, v-lists, the slow and
+// overflow lists) must hold ids < cap (and a bucket entry a source in its slice, a v-list entry a target in its
+// slice). They always do; if one did not, it is skipped (never dereferenced) and its flag is OR-ed into the forest's
+// error word, which the next synchronising call reports as GCC_E_INTERNAL naming the list. One compare per entry.
+constexpr u32 kErrP2 = 2, kErrP3 = 4, kErrSlow = 8, kErrOvf = 16;
+__device__ __forceinline__ void flag_err(u32* err, u32 f) { atomicOr(err, f); }
+
 // ---- layout from a strided sample: capacity = 1.25 x the estimated count + slack, for the buckets (by source
 // slice) and the v-lists (by target slice). One block. The sums are bounded by storage_edges() (host) whatever
 // the sample says; a batch the sample misjudges only overflows (overflow list / inline hooks: still exact).
@@ -132,6 +139,7 @@ __device__ __forceinline__ void block_prefix(const u32* cap, u64* base, u32 ns, 
 
 __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                               Meta* __restrict__ m, u32 bk_blocks, u32 vl_blocks) {
+    trace_start(kTrBkLayout);
     __shared__ u32 s_cu[kMaxSlicesLds], s_cv[kMaxSlicesLds];
     __shared__ u64 s_scan[1024];
     for (u32 s = threadIdx.x; s < ns; s += 1024) s_cu[s] = s_cv[s] = 0;
@@ -201,7 +209,10 @@ template <int P1B, int P1P>
 __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                           Meta* __restrict__ m, u64* __restrict__ bk,
                                                           u64* __restrict__ ovf, u32 ovf_cap, u32* __restrict__ err) {
-    __shared__ u64 s_srt[(P1B * P1P)];
+    trace_start(kTrBkP1);
+    // the tile in bucket order: dynamic LDS (P1B * P1P u64, 64 / 128 KiB), set up like every kernel's LDS beyond
+    // 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-slice state below is static
+    extern __shared__ __attribute__((aligned(16))) u64 s_srt[];
     __shared__ u32 s_cnt[kMaxSlicesLds], s_start[kMaxSlicesLds], s_cap[kMaxSlicesLds];
     __shared__ u32 s_cpos[kMaxSlicesLds], s_cend[kMaxSlicesLds], s_p1[kMaxSlicesLds], s_l1[kMaxSlicesLds],
         s_p2[kMaxSlicesLds], s_l2[kMaxSlicesLds];
@@ -215,6 +226,11 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
         s_base[s] = m->bk_base[s];
         s_cpos[s] = s_cend[s] = 0;  // no chunk yet
     }
+    // Every thread reads every slice's state below — in the tile loop after its barriers, but a block with no
+    // tile goes straight to the chunk-tail loop at the end. Without this barrier such a block read s_cpos / s_cend
+    // / s_base before their owner threads had written them: LDS left over from the previous kernel on the CU, a
+    // wild store address, and (intermittently, small batches only: C4 gives every block tiles) a GPU memory fault.
+    __syncthreads();
     const u64 n2 = n / 2;                                  // whole pairs
     const u64 ntiles = (n2 * 2 + (P1B * P1P) - 1) / (P1B * P1P);
     constexpr int kQ = P1P / 2;
@@ -329,7 +345,8 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                                                                 Meta* __restrict__ m, u32* __restrict__ vl, u32 cps,
                                                                 u32 frac, u32 work_slot, u32 drain_at,
                                                                 const u32* __restrict__ giant, u64* __restrict__ slow,
-                                                                u32 slow_cap) {
+                                                                u32 slow_cap, u32 cap, u32* __restrict__ err) {
+    trace_start(FINAL ? kTrBkP2 : kTrBkP2Seed);
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     u32* s_bits = s_dyn;                                   // kSliceWords
     u32* s_vt = s_dyn + kSliceWords;                       // kP2Round
@@ -405,6 +422,14 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 in[2 * k] = j < np && !(skip_first && j == 0) && ua[2 * k] != 0xFFFFFFFFu;  // UNSEEN: a chunk tail
                 in[2 * k + 1] = j < np && !(skip_last && j == np - 1) && ua[2 * k + 1] != 0xFFFFFFFFu;
             }
+            u32 bad = 0;
+#pragma unroll
+            for (int k = 0; k < kP2Per; ++k)  // a bucket entry: source in this slice, both ids < cap
+                if (in[k] && ((ua[k] >> kSliceBits) != sl || ua[k] >= cap || va[k] >= cap)) {
+                    in[k] = false;
+                    bad = 1;
+                }
+            if (bad) flag_err(err, kErrP2);
             if (p0 + kP2Round / 2 < np) load_round(p0 + kP2Round / 2);  // next round in flight
             bool emit[kP2Per];
             u32 slow_m = 0;  // FINAL: this lane's slow edges (source not in C), bit k
@@ -486,7 +511,9 @@ constexpr int kP3Q = 4;
 template <bool FINAL>
 __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ bits, u32* __restrict__ out,
                                                               u32 nwords32, u32 ns, Meta* __restrict__ m,
-                                                              const u32* __restrict__ vl, u32 cps, u32 work_slot) {
+                                                              const u32* __restrict__ vl, u32 cps, u32 work_slot,
+                                                              u32 cap, u32* __restrict__ err) {
+    trace_start(FINAL ? kTrBkP3 : kTrBkP3Seed);
     extern __shared__ __attribute__((aligned(16))) u32 s_bits[];  // kSliceWords
     __shared__ u32 s_item, s_min;
     typedef u32 u4 __attribute__((ext_vector_type(4)));
@@ -503,6 +530,10 @@ __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ 
     };
     auto visit = [&](u32 v, u32 sbase) {
         if (v == 0xFFFFFFFFu) return;  // a chunk tail (P2)
+        if (v >= cap || v - sbase >= kSliceIds) {  // a v-list entry: target in this slice, < cap
+            flag_err(err, kErrP3);
+            return;
+        }
         const u32 x = v - sbase, msk = 1u << (x & 31);
         if (s_bits[x >> 5] & msk) return;                  // already in C (or taken by this block)
         if (atomicOr(&s_bits[x >> 5], msk) & msk) return;  // another lane of the block took it
@@ -566,6 +597,7 @@ __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ 
 __global__ __launch_bounds__(kBlock) void bucket_hook_kernel(u32* __restrict__ parent, u32* __restrict__ bits,
                                                              u32* __restrict__ nbits, u32 nwords32,
                                                              const u32* __restrict__ giant) {
+    trace_start(kTrBkHook);
     const u32 g = *giant;
     for (u64 w = (u64)blockIdx.x * kBlock + threadIdx.x; w < nwords32; w += (u64)gridDim.x * kBlock) {
         u32 d = nbits[w];
@@ -588,7 +620,9 @@ __global__ __launch_bounds__(kBlock) void bucket_hook_kernel(u32* __restrict__ p
 // g; one end -> the other hooked under g; neither -> united.
 __global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ parent, const u64* __restrict__ slow,
                                                              u32 slow_cap, const Meta* __restrict__ m, u32 nblocks,
-                                                             const u32* __restrict__ bits, const u32* __restrict__ giant) {
+                                                             const u32* __restrict__ bits, const u32* __restrict__ giant,
+                                                             u32 cap, u32* __restrict__ err) {
+    trace_start(kTrBkSlow);
     const u32 g = *giant;
     NoCount c;
     const u64 total = (u64)nblocks * slow_cap;
@@ -597,6 +631,10 @@ __global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ p
         if (k >= m->slow_cnt[r]) continue;
         const u64 e = slow[i];
         const u32 a = (u32)e, b = (u32)(e >> 32);
+        if (a >= cap || b >= cap) {
+            flag_err(err, kErrSlow);
+            continue;
+        }
         const u32 ia = lds_bit(bits, a), ib = lds_bit(bits, b);
         if (ia & ib) continue;
         if (ia) hook_g(parent, g, b);
@@ -609,6 +647,7 @@ __global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ p
 // same deterministic election as the seeded fold), C := {h}, gmin := h. One block.
 __global__ __launch_bounds__(kHubBlock) void bucket_hub_kernel(const u64* __restrict__ edges, u64 n, u32 cap,
                                                                u32* __restrict__ bits, Meta* __restrict__ m) {
+    trace_start(kTrBkHub);
     extern __shared__ __attribute__((aligned(16))) u32 s_tab[];
     u64 e[kHubPer];
     hub_sample(edges, n < kHubSample ? n : kHubSample, e);
@@ -624,6 +663,7 @@ __global__ __launch_bounds__(kHubBlock) void bucket_hub_kernel(const u64* __rest
 __global__ __launch_bounds__(kBlock) void bucket_init_kernel(u32* __restrict__ parent, u32 n,
                                                              const u32* __restrict__ bits, const Meta* __restrict__ m,
                                                              u32* __restrict__ giant) {
+    trace_start(kTrBkInit);
     const u32 g = m->gmin;
     if (blockIdx.x == 0 && threadIdx.x == 0) *giant = g;
     typedef u32 u4 __attribute__((ext_vector_type(4)));
@@ -652,12 +692,17 @@ __global__ __launch_bounds__(kBlock) void bucket_rest_kernel(u32* __restrict__ p
                                                              const u32* __restrict__ bits,
                                                              const u64* __restrict__ edges, u64 n, u32 cap,
                                                              u32* __restrict__ err) {
+    trace_start(kTrBkRest);
     NoCount c;
     const u64 stride = (u64)gridDim.x * kBlock;
     const u64 no = m->ovf_cur < ovf_cap ? m->ovf_cur : ovf_cap;
     for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < no; i += stride) {
         const u64 e = ovf[i];
         const u32 a = (u32)e, b = (u32)(e >> 32);
+        if (a >= cap || b >= cap) {
+            flag_err(err, kErrOvf);
+            continue;
+        }
         if (lds_bit(bits, a) & lds_bit(bits, b)) continue;
         UF::unite(parent, a, b, c);
     }

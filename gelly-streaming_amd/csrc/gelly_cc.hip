@@ -28,6 +28,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -93,10 +94,33 @@ __device__ __forceinline__ bool edge_ok(u32& a, u32& b, u32 cap, u32* err) {
     return ok;
 }
 
+// Kernel-start trace (diagnostics, always on): block 0's thread 0 of each traced kernel stores the kernel's id into
+// one pinned host word (system scope, a vector store). A stream's kernels start in order and a fault stops its
+// queue, so after an asynchronous fault the word names the kernel that faulted (or one of another stream).
+__device__ u32* gcc_trace_slot = nullptr;
+enum : u32 {
+    kTrFold = 1, kTrFiltered, kTrCompressBits, kTrCompressInc, kTrSeedBfs, kTrSeedPack, kTrMergeLabels,
+    kTrBkLayout, kTrBkP1, kTrBkHub, kTrBkP2Seed, kTrBkP3Seed, kTrBkInit, kTrBkP2, kTrBkP3, kTrBkHook, kTrBkSlow, kTrBkRest,
+    kTrCount
+};
+static const char* const kTraceNames[kTrCount] = {
+    "none", "fold_kernel", "fold_filtered_kernel", "compress_bits_kernel", "compress_inc_kernel", "seed_bfs_kernel",
+    "seed_pack_kernel", "merge_labels_kernel", "bucket_layout_kernel", "bucket_kernel (P1)", "bucket_hub_kernel",
+    "slice_filter_kernel<false> (P2 seed)", "slice_hook_kernel<false> (P3 seed)", "bucket_init_kernel",
+    "slice_filter_kernel<true> (P2)", "slice_hook_kernel<true> (P3)", "bucket_hook_kernel", "bucket_slow_kernel",
+    "bucket_rest_kernel"};
+__device__ __forceinline__ void trace_start(u32 id) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        u32* t = gcc_trace_slot;
+        if (t) __hip_atomic_store(t, id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 template <bool REC>
 __global__ __launch_bounds__(kBlock) void fold_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
                                                       u64 n_edges, u32* __restrict__ bloom, u32 cap,
                                                       u32* __restrict__ err) {
+    trace_start(kTrFold);
     NoCount c;
     const u64 stride = (u64)gridDim.x * kBlock;
     for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n_edges; i += stride) {
@@ -245,6 +269,7 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
                                                               const u32* __restrict__ giant,
                                                               u32* __restrict__ slow_count, u32 drain_at, u32 cap,
                                                               u32* __restrict__ err) {
+    trace_start(kTrFiltered);
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     __shared__ u32 s_slow;
     const u32 bitmap_u32 = LDS ? nwords * 2 : 0;  // nwords = u64 words, even
@@ -385,6 +410,7 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
 // (compressed or not) — its (key, parent) pairs generate its partition (DisjointSet.merge :132-136).
 __global__ __launch_bounds__(kBlock) void merge_labels_kernel(u32* __restrict__ parent, const u32* __restrict__ labels,
                                                               u32 n) {
+    trace_start(kTrMergeLabels);
     NoCount c;
     const u64 stride = (u64)gridDim.x * kBlock;
     for (u64 vv = (u64)blockIdx.x * kBlock + threadIdx.x; vv < n; vv += stride) {
@@ -395,18 +421,13 @@ __global__ __launch_bounds__(kBlock) void merge_labels_kernel(u32* __restrict__ 
     }
 }
 
-// Canonicalise: labels[v] := root(v) = min id of v's component, UNSEEN stays UNSEEN (multi-level pointer
-// jumping). Out of place on purpose: the path-splitting stores that let all threads collapse a deep chain
-// together (O(log d) instead of O(d) per thread) write intermediate ancestors into parent[], and such a store
-// can land after another thread's final root store — in place that would leave a vertex pointing at a
-// non-root. labels[] is written exactly once per slot, by its own thread, so it is race-free; parent[] only
-// needs to stay a valid forest (every store is an ancestor, roots never move: no hook is in flight).
-// Algorithmic traffic: 4 B read + 4 B write per id (chain reads hit L2).
-__global__ __launch_bounds__(kBlock) void compress_kernel(u32* __restrict__ parent, u32* __restrict__ labels, u32 n) {
-    const u64 stride = (u64)gridDim.x * kBlock;
-    for (u64 vv = (u64)blockIdx.x * kBlock + threadIdx.x; vv < n; vv += stride)
-        labels[vv] = gcc::compress_label(parent, (u32)vv);  // root / UNSEEN: itself
-}
+// Canonicalise (compress_bits_kernel below): labels[v] := root(v) = min id of v's component, UNSEEN stays UNSEEN
+// (multi-level pointer jumping). Out of place on purpose: the path-splitting stores that let all threads collapse a
+// deep chain together (O(log d) instead of O(d) per thread) write intermediate ancestors into parent[], and such a
+// store can land after another thread's final root store — in place that would leave a vertex pointing at a
+// non-root (the race, replayed in tests/cpp/test_uf_replay.cpp). labels[] is written exactly once per
+// slot, by its own lane, so it is race-free; parent[] only needs to stay a valid forest (every store is an
+// ancestor, roots never move: no hook is in flight). Algorithmic traffic: 4 B read + 4 B write per id.
 
 // Majority vote (Boyer-Moore in its associative pair form) over the labels of 4096 pseudo-random seen ids:
 // the winner is the giant component's label whenever one component holds most of the seen ids. Any
@@ -483,35 +504,94 @@ __global__ __launch_bounds__(1024) void giant_vote_kernel(u32* __restrict__ pare
 
 // Compress fused with the giant bitmap: labels[v] = root(v) as compress_kernel, and bits[w] bit b =
 // (labels[64w + b] == g) where g = the current root of the tracked component (the root of giant_prev: roots
-// only move to smaller ids, so following the old root finds the same, grown, component). One u64 bitmap word
-// per wave via ballot. giant_next receives g. Grid-stride in whole waves so the ballot covers 64 ids.
+// only move to smaller ids, so following the old root finds the same, grown, component). giant_next receives g.
+// A wave labels 256-id chunks, 4 ids per lane (16-B loads and stores), kBitsU chunks in flight per wave before any
+// is labelled (one id per lane and one load at a time kept too little in flight: C4's 64M ids at ~1.9 TB/s); the
+// lanes' 4-bit nibbles are OR-ed into the chunk's 4 bitmap words. labels == nullptr: a mid-fold refresh of the
+// bitmap alone (refresh_now); bits == nullptr (the filter off): the labels alone. Prefetched parent values are historically valid (splitting stores only write
+// ancestors), so a find from one is exact.
+constexpr int kBitsU = 4;
+__device__ __forceinline__ void chunk_bits(u64* bits, u64 nwords, u64 ch, u32 lane, u32 g, const u32 (&lab)[4]) {
+    u64 w = 0;
+    if (g != UNSEEN)
+        w = (u64)((lab[0] == g) | ((lab[1] == g) << 1) | ((lab[2] == g) << 2) | ((lab[3] == g) << 3)) << (4 * (lane & 15));
+    w |= __shfl_xor(w, 1, 64);
+    w |= __shfl_xor(w, 2, 64);
+    w |= __shfl_xor(w, 4, 64);
+    w |= __shfl_xor(w, 8, 64);
+    const u64 wi = ch * 4 + (lane >> 4);
+    if ((lane & 15) == 0 && wi < nwords) bits[wi] = w;
+}
+
+static inline unsigned chunk_grid(u64 n, int per_wave, int block, unsigned max_blocks) {  // waves for 256-id chunks
+    const u64 waves = ((n + 255) / 256 + per_wave - 1) / per_wave;
+    const u64 b = (waves * 64 + block - 1) / block;
+    return (unsigned)(b < 1 ? 1 : (b > max_blocks ? max_blocks : b));
+}
+
 __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__ parent, u32* __restrict__ labels, u32 n,
                                                                const u32* __restrict__ giant_prev,
                                                                u32* __restrict__ giant_next, u64* __restrict__ bits,
                                                                u32* __restrict__ bloom_clear) {
+    trace_start(kTrCompressBits);
     __shared__ u32 s_g;
     NoCount c;
+    const u32 lane = threadIdx.x & 63;
+    const u64 nwords = ((u64)n + 63) / 64;
+    const u64 nfull = (u64)n / 256;
+    const u64 nwaves = (u64)gridDim.x * (kBlock / 64);
+    const u64 wave = (u64)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    u32x4 pv[kBitsU];
+    auto load_batch = [&](u64 base) {
+#pragma unroll
+        for (int k = 0; k < kBitsU; ++k) {  // clamped, unconditional: countable loads
+            const u64 ch = base + (u64)k * nwaves;
+            pv[k] = *reinterpret_cast<const u32x4*>(parent + (ch < nfull ? ch : nfull - 1) * 256 + 4 * lane);
+        }
+    };
+    if (wave < nfull) load_batch(wave);
     if (bloom_clear)  // the bloom buffer the next fold records into (compress_inc_kernel)
         for (u32 w = blockIdx.x * kBlock + threadIdx.x; w < gcc::kBloomBits / 32; w += gridDim.x * kBlock) bloom_clear[w] = 0;
     if (threadIdx.x == 0) {
-        const u32 g0 = *giant_prev;
+        const u32 g0 = giant_prev ? *giant_prev : UNSEEN;
         s_g = (g0 == UNSEEN) ? UNSEEN : UF::find_from(parent, g0, parent[g0], c);
-        if (blockIdx.x == 0) *giant_next = s_g;
+        if (blockIdx.x == 0 && giant_next) *giant_next = s_g;
     }
     __syncthreads();
     const u32 g = s_g;
-    const u64 stride = (u64)gridDim.x * kBlock;
-    const u64 end = ((u64)n + 63) / 64 * 64;
-    for (u64 vv = (u64)blockIdx.x * kBlock + threadIdx.x; vv < end; vv += stride) {
-        u32 lab = UNSEEN;
-        if (vv < n) {
-            const u32 v = (u32)vv;
-            const u32 p = parent[v];
-            lab = (p >= v) ? p : UF::find_from(parent, v, p, c);
-            if (labels) labels[v] = lab;  // null: a mid-fold refresh of the bitmap alone (refresh_now)
+    for (u64 base = wave; base < nfull; base += (u64)kBitsU * nwaves) {
+        u32x4 cur[kBitsU];
+#pragma unroll
+        for (int k = 0; k < kBitsU; ++k) cur[k] = pv[k];
+        const u64 nb = base + (u64)kBitsU * nwaves;
+        if (nb < nfull) load_batch(nb);  // wave-uniform
+#pragma unroll
+        for (int k = 0; k < kBitsU; ++k) {
+            const u64 ch = base + (u64)k * nwaves;
+            if (ch >= nfull) break;  // wave-uniform
+            const u32 v0 = (u32)(ch * 256 + 4 * lane);
+            const u32x4 p = cur[k];
+            u32 lab[4];
+            lab[0] = (p.x >= v0) ? p.x : UF::find_from(parent, v0, p.x, c);
+            lab[1] = (p.y >= v0 + 1) ? p.y : UF::find_from(parent, v0 + 1, p.y, c);
+            lab[2] = (p.z >= v0 + 2) ? p.z : UF::find_from(parent, v0 + 2, p.z, c);
+            lab[3] = (p.w >= v0 + 3) ? p.w : UF::find_from(parent, v0 + 3, p.w, c);
+            if (labels) {
+                const u32x4 o = {lab[0], lab[1], lab[2], lab[3]};
+                *reinterpret_cast<u32x4*>(labels + v0) = o;
+            }
+            if (bits) chunk_bits(bits, nwords, ch, lane, g, lab);
         }
-        const unsigned long long m = __ballot(g != UNSEEN && lab == g);
-        if ((threadIdx.x & 63) == 0) bits[vv >> 6] = m;
+    }
+    if (nfull * 256 < n && wave == nfull % nwaves) {  // the partial last chunk: id by id
+        const u64 v0 = nfull * 256 + 4 * lane;
+        u32 lab[4] = {UNSEEN, UNSEEN, UNSEEN, UNSEEN};
+        for (u32 k = 0; k < 4; ++k)
+            if (v0 + k < n) {
+                lab[k] = gcc::compress_label(parent, (u32)(v0 + k));
+                if (labels) labels[v0 + k] = lab[k];
+            }
+        if (bits) chunk_bits(bits, nwords, nfull, lane, g, lab);
     }
 }
 
@@ -522,6 +602,7 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
 // bloom in LDS; a lane reads 4 consecutive ids (16 B) and a wave covers 256 ids = 4 bitmap words of the
 // tracked component (as compress_bits_kernel). The block also clears its share of the other bloom buffer.
 constexpr int kIncBlock = 1024;
+constexpr int kIncU = 4;  // 256-id chunks per wave in flight
 using gcc::inc_label;  // uf_device.h: shared with the host replay
 
 // INPLACE: labels == parent. parent[] is already canonical except where a marked parent needs the find, so only
@@ -535,9 +616,25 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
                                                                  u32* __restrict__ bloom_clear,
                                                                  const u32* __restrict__ giant_prev,
                                                                  u32* __restrict__ giant_next, u64* __restrict__ bits) {
+    trace_start(kTrCompressInc);
     extern __shared__ __attribute__((aligned(16))) u32 s_bloom[];
     __shared__ u32 s_g;
     constexpr u32 kW4 = gcc::kBloomBits / 128;  // bloom size in 16-B words
+    const u32 lane = threadIdx.x & 63;
+    const u64 nwords = ((u64)n + 63) / 64;
+    const u64 nfull = (u64)n / 256;  // whole 256-id chunks (one 16-B load per lane); the partial tail: below
+    const u64 nwaves = (u64)gridDim.x * (kIncBlock / 64);
+    const u64 wave = (u64)blockIdx.x * (kIncBlock / 64) + (threadIdx.x >> 6);
+    // the first batch of parent[] loads is issued before the bloom's LDS fill and lands behind it
+    u32x4 pv[kIncU];
+    auto load_batch = [&](u64 base) {
+#pragma unroll
+        for (int k = 0; k < kIncU; ++k) {  // clamped, unconditional: the compiler can count them
+            const u64 ch = base + (u64)k * nwaves;
+            pv[k] = *reinterpret_cast<const u32x4*>(parent + (ch < nfull ? ch : nfull - 1) * 256 + 4 * lane);
+        }
+    };
+    if (wave < nfull) load_batch(wave);
     {
         const u32x4* src = reinterpret_cast<const u32x4*>(bloom);
         u32x4* dst = reinterpret_cast<u32x4*>(s_bloom);
@@ -554,17 +651,21 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
     }
     __syncthreads();
     const u32 g = s_g;
-    const u32 lane = threadIdx.x & 63;
-    const u64 nwords = ((u64)n + 63) / 64;
-    const u64 nchunks = ((u64)n + 255) / 256;
-    const u64 nwaves = (u64)gridDim.x * (kIncBlock / 64);
-    // (a 4-chunk software pipeline of the parent[] loads measured slower on C5: the finds of relabelled ids,
-    // not the stream, bound this pass there; profiles/r1_sweep_inc_inplace.log)
-    for (u64 ch = (u64)blockIdx.x * (kIncBlock / 64) + (threadIdx.x >> 6); ch < nchunks; ch += nwaves) {
-        const u64 v0 = ch * 256 + 4 * lane;
-        u32 lab[4] = {UNSEEN, UNSEEN, UNSEEN, UNSEEN};
-        if (v0 + 3 < n) {
-            const u32x4 p = *reinterpret_cast<const u32x4*>(parent + v0);
+    // kIncU chunks per wave in flight (one 16-B load each) before any is labelled: a wave that waited for each
+    // chunk in turn kept ~4 MB in flight device-wide and streamed C5's 64 MB parent[] at ~2.2 TB/s
+    for (u64 base = wave; base < nfull; base += (u64)kIncU * nwaves) {
+        u32x4 cur[kIncU];
+#pragma unroll
+        for (int k = 0; k < kIncU; ++k) cur[k] = pv[k];
+        const u64 nb = base + (u64)kIncU * nwaves;
+        if (nb < nfull) load_batch(nb);  // wave-uniform: the next batch streams in while this one is labelled
+#pragma unroll
+        for (int k = 0; k < kIncU; ++k) {
+            const u64 ch = base + (u64)k * nwaves;
+            if (ch >= nfull) break;  // wave-uniform
+            const u64 v0 = ch * 256 + 4 * lane;
+            const u32x4 p = cur[k];
+            u32 lab[4];
             lab[0] = inc_label(parent, s_bloom, (u32)v0, p.x);
             lab[1] = inc_label(parent, s_bloom, (u32)v0 + 1, p.y);
             lab[2] = inc_label(parent, s_bloom, (u32)v0 + 2, p.z);
@@ -578,24 +679,19 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
                 const u32x4 o = {lab[0], lab[1], lab[2], lab[3]};
                 *reinterpret_cast<u32x4*>(labels + v0) = o;
             }
-        } else {
-            for (u32 k = 0; k < 4; ++k)
-                if (v0 + k < n) {
-                    const u32 pk = parent[v0 + k];
-                    lab[k] = inc_label(parent, s_bloom, (u32)(v0 + k), pk);
-                    if (!INPLACE || lab[k] != pk) labels[v0 + k] = lab[k];
-                }
+            chunk_bits(bits, nwords, ch, lane, g, lab);
         }
-        u64 w = 0;
-        if (g != UNSEEN)
-            w = (u64)((lab[0] == g) | ((lab[1] == g) << 1) | ((lab[2] == g) << 2) | ((lab[3] == g) << 3))
-                << (4 * (lane & 15));
-        w |= __shfl_xor(w, 1, 64);
-        w |= __shfl_xor(w, 2, 64);
-        w |= __shfl_xor(w, 4, 64);
-        w |= __shfl_xor(w, 8, 64);
-        const u64 wi = ch * 4 + (lane >> 4);
-        if ((lane & 15) == 0 && wi < nwords) bits[wi] = w;
+    }
+    if (nfull * 256 < n && wave == nfull % nwaves) {  // the partial last chunk: id by id
+        const u64 v0 = nfull * 256 + 4 * lane;
+        u32 lab[4] = {UNSEEN, UNSEEN, UNSEEN, UNSEEN};
+        for (u32 k = 0; k < 4; ++k)
+            if (v0 + k < n) {
+                const u32 pk = parent[v0 + k];
+                lab[k] = inc_label(parent, s_bloom, (u32)(v0 + k), pk);
+                if (!INPLACE || lab[k] != pk) labels[v0 + k] = lab[k];
+            }
+        chunk_bits(bits, nwords, nfull, lane, g, lab);
     }
 }
 
@@ -750,6 +846,7 @@ __global__ __launch_bounds__(BLOCK) void seed_bfs_kernel(const u64* __restrict__
                                                          const u32* __restrict__ bits32, u32 nwords32,
                                                          u8* __restrict__ flags, u32* __restrict__ bmin, u8 epoch,
                                                          u32 cap, u32* __restrict__ err) {
+    trace_start(kTrSeedBfs);
     static_assert(!HUB || (LDS && BLOCK == kHubBlock), "the fused hub election needs the LDS variant");
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     __shared__ u32 s_min;
@@ -844,6 +941,7 @@ template <bool PARENT>
 __global__ __launch_bounds__(kBlock) void seed_pack_kernel(u32* __restrict__ parent, u32 n, const u8* __restrict__ flags,
                                                            u32* __restrict__ bits32, const u32* __restrict__ bmin,
                                                            u32 n_bmin, u32* __restrict__ giant, u8 epoch) {
+    trace_start(kTrSeedPack);
     u32 g = 0;
     if constexpr (PARENT) {  // g = min C = the minimum of the BFS blocks' (and the hub's) slots
         __shared__ u32 s_g[kBlock / 64];
@@ -1314,6 +1412,15 @@ static void mark_mutated(gcc_forest* h, bool recorded = false) {
 // start/stop events, which the runtime records from the dispatch itself: the logged duration is the kernel's
 // own execution, and no extra packets (hipEventRecord markers cost ~4 us each between dependent kernels) are
 // put between the pipeline's launches.
+// GELLY_SYNC_EACH=1 (diagnostics): synchronise after every launch, so that an asynchronous fault names its kernel.
+static bool sync_each_launch() {
+    static const bool on = [] {
+        const char* e = std::getenv("GELLY_SYNC_EACH");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
 template <typename F, typename... Args>
 static int launch_k(gcc_forest* h, const char* name, u64 edges, F kernel, dim3 grid, dim3 block, size_t shmem,
                     Args... args) {
@@ -1337,6 +1444,10 @@ static int launch_k(gcc_forest* h, const char* name, u64 edges, F kernel, dim3 g
         h->klog.push_back({name, ev, edges});
     }
     HIP_TRY(hipGetLastError());
+    if (sync_each_launch()) {  // diagnostics: a fault is reported by the launch that caused it
+        const hipError_t e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return set_err(GCC_E_HIP, "kernel %s: %s", name, hipGetErrorString(e));
+    }
     return GCC_OK;
 }
 
@@ -1346,8 +1457,13 @@ static int stream_sync_checked(gcc_forest* h) {
     HIP_TRY(hipMemcpyAsync(h->h_err, h->d_err, sizeof(u32), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (*h->h_err) {
+        const u32 e = *h->h_err;
         *h->h_err = 0;
         HIP_TRY(hipMemsetAsync(h->d_err, 0, sizeof(u32), h->stream));
+        if (e & ~1u)  // bucket_fold.h's internal checks (kErr*): an entry of an internal list was out of range
+            return set_err(GCC_E_INTERNAL, "bucketed fold consistency check failed (flags 0x%x: %s%s%s%s)", e,
+                           (e & bk::kErrP2) ? "P2 bucket entry " : "", (e & bk::kErrP3) ? "P3 v-list entry " : "",
+                           (e & bk::kErrSlow) ? "slow-list entry " : "", (e & bk::kErrOvf) ? "overflow entry" : "");
         return set_err(GCC_E_INVALID, "a device batch held a vertex id >= id_capacity %u (those edges were skipped)",
                        h->cap);
     }
@@ -1383,8 +1499,8 @@ static int compress_now(gcc_forest* h, const char* name = "compress") {
     bool inplace = false;  // the compress rewrote d_parent itself (no swap)
     const bool inc_here = inc_forest(h);
     if (!h->filter_enabled()) {
-        rc = launch_k(h, name, 0, compress_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->d_parent,
-                      h->d_spare, h->cap);
+        rc = launch_k(h, name, 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)), dim3(kBlock), 0,
+                      h->d_parent, h->d_spare, h->cap, (const u32*)nullptr, (u32*)nullptr, (u64*)nullptr, (u32*)nullptr);
     } else {
         rc = alloc_filter(h);
         if (rc) return rc;
@@ -1409,7 +1525,7 @@ static int compress_now(gcc_forest* h, const char* name = "compress") {
                                     (const u32*)h->bloom(h->bloom_cur), clear, (const u32*)(h->d_giant + h->giant_slot),
                                     h->d_giant + (h->giant_slot ^ 1), h->d_bits);
         } else if (!rc) {
-            rc = launch_k(h, name, 0, compress_bits_kernel, dim3(grid_for(h->nwords() * 64ull, kMaxGrid)), dim3(kBlock), 0,
+            rc = launch_k(h, name, 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)), dim3(kBlock), 0,
                           h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
                           h->d_giant + (h->giant_slot ^ 1), h->d_bits, clear);
         }
@@ -1435,7 +1551,7 @@ static int refresh_now(gcc_forest* h) {
         rc = launch_k(h, "vote", 0, giant_vote_kernel, dim3(1), dim3(1024), 0, h->d_parent, h->cap,
                       h->d_giant + h->giant_slot, h->d_giant + 4);
     if (!rc)
-        rc = launch_k(h, "refresh_bits", 0, compress_bits_kernel, dim3(grid_for(h->nwords() * 64ull, kMaxGrid)),
+        rc = launch_k(h, "refresh_bits", 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)),
                       dim3(kBlock), 0, h->d_parent, (u32*)nullptr, h->cap, (const u32*)(h->d_giant + h->giant_slot),
                       h->d_giant + (h->giant_slot ^ 1), h->d_bits, (u32*)nullptr);
     if (rc) return rc;
@@ -1602,13 +1718,27 @@ static bool bucket_applies(const gcc_forest* h, const u32* d_pairs, u64 n) {
              reinterpret_cast<uintptr_t>(h->d_spare)) & 15) == 0;
 }
 
+// GELLY_POISON=1 (diagnostics): the bucketed fold's scratch buffers start as 0xA5 bytes instead of whatever the
+// allocator hands back, so that a read of an entry no kernel wrote trips the kErr* checks deterministically.
+static bool poison_scratch() {
+    static const bool on = [] {
+        const char* e = std::getenv("GELLY_POISON");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
 template <typename T>
-static int grow(T*& p, u64& cap, u64 need) {
+static int grow(T*& p, u64& cap, u64 need, hipStream_t st) {
     if (cap >= need) return GCC_OK;
-    if (p) HIP_TRY(hipFree(p));
+    if (p) {
+        HIP_TRY(hipStreamSynchronize(st));  // the stream's earlier launches may still read the old buffer
+        HIP_TRY(hipFree(p));
+    }
     p = nullptr;
     cap = 0;
     HIP_TRY(hipMalloc((void**)&p, (size_t)need * sizeof(T)));
+    if (poison_scratch()) HIP_TRY(hipMemsetAsync(p, 0xA5, (size_t)need * sizeof(T), st));  // stream-ordered
     cap = need;
     return GCC_OK;
 }
@@ -1619,14 +1749,17 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     int rc = alloc_filter(h);
     if (rc) return rc;
     const u32 ns = bucket_slices(h);
-    if (!h->d_meta) HIP_TRY(hipMalloc((void**)&h->d_meta, sizeof(bk::Meta)));
+    if (!h->d_meta) {
+        HIP_TRY(hipMalloc((void**)&h->d_meta, sizeof(bk::Meta)));
+        if (poison_scratch()) HIP_TRY(hipMemsetAsync(h->d_meta, 0xA5, sizeof(bk::Meta), h->stream));
+    }
     const u32 p1_blocks = 2 * (u32)h->n_cu;  // (bucket_p1 = 1 runs n_cu blocks: fewer writers, same slack bound)
     const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
-    if ((rc = grow(h->d_bk, h->bk_cap_edges, bk::storage_edges(n, ns, p1_blocks)))) return rc;
-    if ((rc = grow(h->d_ovf, h->ovf_cap, n / 8 + 65536))) return rc;
-    if ((rc = grow(h->d_vl, h->vl_cap, bk::storage_edges(n, ns, p2_blocks)))) return rc;
+    if ((rc = grow(h->d_bk, h->bk_cap_edges, bk::storage_edges(n, ns, p1_blocks), h->stream))) return rc;
+    if ((rc = grow(h->d_ovf, h->ovf_cap, n / 8 + 65536, h->stream))) return rc;
+    if ((rc = grow(h->d_vl, h->vl_cap, bk::storage_edges(n, ns, p2_blocks), h->stream))) return rc;
     const u32 slow_cap = (u32)std::min<u64>(0x7FFFFFFFull, std::max<u64>(4096, n / p2_blocks / 8));
-    if ((rc = grow(h->d_slow, h->slow_cap_total, (u64)p2_blocks * slow_cap))) return rc;
+    if ((rc = grow(h->d_slow, h->slow_cap_total, (u64)p2_blocks * slow_cap, h->stream))) return rc;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
     u32* bits = reinterpret_cast<u32*>(h->d_bits);
     const u32 nw32 = 2 * (h->nwords() + (h->nwords() & 1));
@@ -1645,10 +1778,10 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                   p1_blocks, p2_blocks);
     if (!rc)
         rc = t.bucket_p1 == 1
-                 ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16>, dim3(h->n_cu), dim3(1024), 0, edges, n, ns, h->cap,
-                            h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err)
-                 : launch_k(h, "bucket", n, bk::bucket_kernel<512, 16>, dim3(p1_blocks), dim3(512), 0, edges, n, ns, h->cap,
-                      h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err);
+                 ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16>, dim3(h->n_cu), dim3(1024), 1024 * 16 * sizeof(u64),
+                            edges, n, ns, h->cap, h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err)
+                 : launch_k(h, "bucket", n, bk::bucket_kernel<512, 16>, dim3(p1_blocks), dim3(512), 512 * 16 * sizeof(u64),
+                            edges, n, ns, h->cap, h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err);
     if (rc) return rc;
     // seeding: C := {hub}, then levels over the sample
     HIP_TRY(hipMemsetAsync(bits, 0, (size_t)nw32 * sizeof(u32), h->stream));
@@ -1661,10 +1794,10 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
         rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
                       f_lds, h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps, frac,
-                      slot++, h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap);
+                      slot++, h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err);
         if (!rc)
             rc = launch_k(h, "seed_hook", 0, bk::slice_hook_kernel<false>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                          bits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++);
+                          bits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
     }
     // parent[] := C ? g : UNSEEN (the reset), then every bucketed edge, the overflow list, a spill
     if (!rc)
@@ -1674,17 +1807,17 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
     rc = launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true>, dim3(p2_blocks), dim3(bk::kP2Block), f_lds,
                   h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps, 65536u, slot++,
-                  h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap);
+                  h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err);
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                      h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++);
+                      h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
     if (!rc)
         rc = launch_k(h, "bucket_hook", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
                       h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
     if (!rc)
         rc = launch_k(h, "bucket_slow", 0, bk::bucket_slow_kernel, dim3(grid_for((u64)p2_blocks * slow_cap, kMaxGrid)),
                       dim3(kBlock), 0, h->d_parent, (const u64*)h->d_slow, slow_cap, (const bk::Meta*)h->d_meta, p2_blocks,
-                      (const u32*)bits, (const u32*)giant);
+                      (const u32*)bits, (const u32*)giant, h->cap, h->d_err);
     if (!rc)
         rc = launch_k(h, "bucket_rest", 0, bk::bucket_rest_kernel, dim3(grid_for(n / 64 + 1, kMaxGrid)), dim3(kBlock), 0,
                       h->d_parent, (const u64*)h->d_ovf, ovf_cap, (const bk::Meta*)h->d_meta, (const u32*)bits, edges, n,
@@ -1925,6 +2058,33 @@ static std::once_flag g_attr_once[kMaxDevices];
 static int g_attr_rc[kMaxDevices];
 static std::string g_attr_msg[kMaxDevices];
 
+// The kernel-start trace word (trace_start): one pinned, device-mapped host word for the process, its address set
+// into gcc_trace_slot once per device (with the LDS attributes).
+static u32* g_trace_host = nullptr;
+static std::once_flag g_trace_once;
+
+extern "C++" const char* gcc_fault_note(hipError_t e) {  // abi_common.h (C++ linkage, inside this extern "C" block)
+    static thread_local char buf[96];
+    if (e != hipErrorIllegalAddress && e != hipErrorLaunchFailure) return "";
+    const u32 id = g_trace_host ? __atomic_load_n(g_trace_host, __ATOMIC_RELAXED) : 0u;
+    snprintf(buf, sizeof(buf), " [last kernel started: %s]", id < kTrCount ? kTraceNames[id] : "?");
+    return buf;
+}
+
+static int set_trace_slot() {  // the current device
+    std::call_once(g_trace_once, [] {
+        if (hipHostMalloc((void**)&g_trace_host, 64, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
+            g_trace_host = nullptr;
+        else
+            *g_trace_host = 0;
+    });
+    if (!g_trace_host) return GCC_OK;  // diagnostics only
+    u32* dev = nullptr;
+    HIP_TRY(hipHostGetDevicePointer((void**)&dev, g_trace_host, 0));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(gcc_trace_slot), &dev, sizeof(dev)));
+    return GCC_OK;
+}
+
 static int set_lds_attrs_impl() {
     const int filtered = (int)(kLdsBitmapMaxWords * sizeof(u64) + (kFilterBlockLds / 64) * kRing * sizeof(u64));
     const int bitmap = (int)(kLdsBitmapMaxWords * sizeof(u64));
@@ -1948,9 +2108,11 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kSliceWords * sizeof(u32))},
         {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kSliceWords * sizeof(u32))},
         {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
+        {(const void*)bk::bucket_kernel<512, 16>, (int)(512 * 16 * sizeof(u64))},
+        {(const void*)bk::bucket_kernel<1024, 16>, (int)(1024 * 16 * sizeof(u64))},
     };
     for (const auto& t : tab) HIP_TRY(hipFuncSetAttribute(t.f, hipFuncAttributeMaxDynamicSharedMemorySize, t.bytes));
-    return GCC_OK;
+    return set_trace_slot();
 }
 
 static int ensure_lds_attrs(int device) {  // `device` is current
@@ -1989,7 +2151,7 @@ static int forest_create_impl(int device, uint32_t id_capacity, uint32_t* d_buf0
     if (e != hipSuccess) return fail(set_err(GCC_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e)));
     h->stream = h->own_stream;
     e = hipMalloc((void**)&h->d_err, sizeof(u32));
-    if (e == hipSuccess) e = hipMemset(h->d_err, 0, sizeof(u32));
+    if (e == hipSuccess) e = hipMemsetAsync(h->d_err, 0, sizeof(u32), h->stream);  // ordered before its kernels
     if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_err, sizeof(u32), hipHostMallocDefault);
     if (e != hipSuccess) return fail(set_err(GCC_E_HIP, "error word: %s", hipGetErrorString(e)));
     *h->h_err = 0;
@@ -2014,6 +2176,8 @@ int gcc_forest_create(int device, uint32_t id_capacity, gcc_forest** out) {
 
 int gcc_forest_create_ext(int device, uint32_t id_capacity, uint32_t* d_buf0, uint32_t* d_buf1, gcc_forest** out) {
     CHECK_ARG(d_buf0 && d_buf1 && d_buf0 != d_buf1, "need two distinct device buffers");
+    CHECK_ARG(((reinterpret_cast<uintptr_t>(d_buf0) | reinterpret_cast<uintptr_t>(d_buf1)) & 15) == 0,
+              "the id-range buffers must be 16-byte aligned (the compress moves 4 ids per 16-B access)");
     return forest_create_impl(device, id_capacity, d_buf0, d_buf1, out);
 }
 

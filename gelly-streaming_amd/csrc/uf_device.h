@@ -11,8 +11,10 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define UF_HD __host__ __device__ __forceinline__
+#define UF_UNROLL _Pragma("unroll")
 #else
 #define UF_HD inline
+#define UF_UNROLL
 #endif
 
 #define GCC_UNSEEN_DEV 0xFFFFFFFFu
@@ -127,15 +129,30 @@ struct Count {
 // p that is some id's parent is still a root: that id's label is p, no find needed. Ids that leave UNSEEN need
 // no mark: one hung straight under a root never becomes a parent value, one made a root is marked if hooked.
 constexpr u32 kBloomBits = 1u << 20;  // 128 KiB: one CU's LDS copy in the incremental compress
-UF_HD u32 bloom_slot(u32 x) { return (x * 0x9E3779B1u) >> 12; }
+// kBloomK bits per mark (independent multiplicative hashes): at C5's 65K marks per window in 1M bits the false-hit
+// rate is 6.0 % with one bit, 1.5 % with two; every false hit costs the compress one random read of parent[p]
+constexpr int kBloomK = 2;
+UF_HD u32 bloom_slot(u32 x, int i) { return (x * (i == 0 ? 0x9E3779B1u : 0x85EBCA77u)) >> 12; }
+UF_HD bool bloom_test(const u32* bloom, u32 x) {
+    bool hit = true;
+    UF_UNROLL
+    for (int i = 0; i < kBloomK; ++i) {
+        const u32 s = bloom_slot(x, i);
+        hit = hit && ((bloom[s >> 5] >> (s & 31)) & 1u);
+    }
+    return hit;
+}
 struct NoRec {
     UF_HD void mark(u32) const {}
 };
 struct BloomRec {
     u32* bloom;
     UF_HD void mark(u32 x) const {
-        const u32 s = bloom_slot(x);
-        aor(&bloom[s >> 5], 1u << (s & 31));
+        UF_UNROLL
+        for (int i = 0; i < kBloomK; ++i) {
+            const u32 s = bloom_slot(x, i);
+            aor(&bloom[s >> 5], 1u << (s & 31));
+        }
     }
 };
 
@@ -276,8 +293,7 @@ UF_HD u32 compress_label(u32* parent, u32 v) {
 // still a root (BloomRec), so labels[v] = p without a find; a marked one takes a read-only find.
 UF_HD u32 inc_label(const u32* parent, const u32* bloom, u32 v, u32 p) {
     if (p >= v) return p;  // root (p == v) or UNSEEN
-    const u32 s = bloom_slot(p);
-    if (!((bloom[s >> 5] >> (s & 31)) & 1u)) return p;
+    if (!bloom_test(bloom, p)) return p;
     NoCount c;
     return UFRead::find_from(const_cast<u32*>(parent), v, p, c);
 }

@@ -45,6 +45,7 @@ extern "C" {
 #define GCC_E_HIP (-2)     /* a HIP runtime call failed */
 #define GCC_E_NODEV (-3)   /* no usable gfx950 device */
 #define GCC_E_OOM (-4)     /* device or pinned-host allocation failed */
+#define GCC_E_INTERNAL (-5) /* a device-side consistency check failed (a bug: the message names the kernel) */
 
 /* ---- generator parameters (synthetic edge streams; see gelly-streaming_amd/csrc/edge_gen.h) ---- */
 enum {
@@ -83,7 +84,8 @@ int gcc_gen_device(const gcc_gen_params* p, uint64_t first, uint64_t count, uint
 int gcc_forest_create(int device, uint32_t id_capacity, gcc_forest** out);
 /* same, over two caller-owned device buffers of id_capacity u32 each (e.g. torch tensors; not freed by
  * destroy). The forest works in one and compress writes the canonical labels into the other, after which they
- * swap roles: gcc_forest_device_ptr tells which one currently holds the forest / labels. */
+ * swap roles: gcc_forest_device_ptr tells which one currently holds the forest / labels. Both must be 16-byte
+ * aligned (GCC_E_INVALID otherwise). */
 int gcc_forest_create_ext(int device, uint32_t id_capacity, uint32_t* d_buf0, uint32_t* d_buf1, gcc_forest** out);
 int gcc_forest_destroy(gcc_forest* h);
 /* order the handle's work on hip_stream (taken literally: NULL = the null stream, e.g. torch's default

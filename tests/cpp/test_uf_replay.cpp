@@ -298,10 +298,8 @@ static void k_compress_inc_inplace(Forest& f, int T, u64 seed) {
             for (u32 k = 0; k < 4; ++k) p[k] = (v0 + k < V) ? gcc::ld(&par[v0 + k]) : U;
             for (u32 k = 0; k < 4; ++k)
                 if (v0 + k < V) {
-                    if (p[k] < v0 + k) {
-                        const u32 sl = gcc::bloom_slot(p[k]);
-                        if ((lds[sl >> 5] >> (sl & 31)) & 1u) n_inc_finds.fetch_add(1, std::memory_order_relaxed);
-                    }
+                    if (p[k] < v0 + k && gcc::bloom_test(lds.data(), p[k]))
+                        n_inc_finds.fetch_add(1, std::memory_order_relaxed);
                     lab[k] = gcc::inc_label(par, lds.data(), v0 + k, p[k]);
                     if (lab[k] != p[k]) gcc::st(&par[v0 + k], lab[k]);
                 }
