@@ -1462,7 +1462,7 @@ static int stream_sync_checked(gcc_forest* h) {
         HIP_TRY(hipMemsetAsync(h->d_err, 0, sizeof(u32), h->stream));
         if (e & ~1u)  // bucket_fold.h's internal checks (kErr*): an entry of an internal list was out of range
             return set_err(GCC_E_INTERNAL, "bucketed fold consistency check failed (flags 0x%x: %s%s%s%s)", e,
-                           (e & bk::kErrP2) ? "P2 bucket entry " : "", (e & bk::kErrP3) ? "P3 v-list entry " : "",
+                           (e & bk::kErrP2) ? "P2 bucket entry " : "", "",
                            (e & bk::kErrSlow) ? "slow-list entry " : "", (e & bk::kErrOvf) ? "overflow entry" : "");
         return set_err(GCC_E_INVALID, "a device batch held a vertex id >= id_capacity %u (those edges were skipped)",
                        h->cap);
