@@ -5,6 +5,8 @@
 //             a generation word with agent-scope atomic loads, fences (acquire)
 //   xcd:      the same, two-level: blocks arrive at their XCD's counter (blockIdx % 8), the last arriver of an XCD
 //             arrives at the top counter
+//   graph:    the K empty kernels captured once into a hipGraph and replayed (is the per-kernel cost a host-side
+//             launch cost that a graph removes, or the GPU's own dispatch + kernel-boundary cost?)
 // The kernel is co-resident by construction (one 1024-thread block per CU, occupancy checked on the host).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 probe_gridbar.hip -o probe_gridbar
 #include <hip/hip_runtime.h>
@@ -98,6 +100,30 @@ int main(int argc, char** argv) {
             CK(hipEventSynchronize(b));
             CK(hipEventElapsedTime(&ms, a, b));
             printf("%s: %d barriers in one kernel   %.3f us each\n", x ? "xcd " : "flat", K, 1000.0 * ms / K);
+        }
+    }
+    {  // the same K empty kernels as one captured graph
+        hipStream_t st;
+        CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        hipGraph_t graph;
+        hipGraphExec_t exec;
+        CK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        for (int k = 0; k < K; ++k) hipLaunchKernelGGL(empty_kernel, dim3(ncu), dim3(1024), 0, st, sink);
+        CK(hipStreamEndCapture(st, &graph));
+        CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        for (int rep = 0; rep < 3; ++rep) {
+            CK(hipEventRecord(a, st));
+            CK(hipGraphLaunch(exec, st));
+            CK(hipEventRecord(b, st));
+            CK(hipEventSynchronize(b));
+            CK(hipEventElapsedTime(&ms, a, b));
+            printf("graph: %d empty kernels in one hipGraph  %.3f us each\n", K, 1000.0 * ms / K);
+            CK(hipEventRecord(a, st));
+            for (int k = 0; k < K; ++k) hipLaunchKernelGGL(empty_kernel, dim3(ncu), dim3(1024), 0, st, sink);
+            CK(hipEventRecord(b, st));
+            CK(hipEventSynchronize(b));
+            CK(hipEventElapsedTime(&ms, a, b));
+            printf("stream (non-blocking): %d empty kernels   %.3f us each\n", K, 1000.0 * ms / K);
         }
     }
     return 0;
