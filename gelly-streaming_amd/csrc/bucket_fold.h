@@ -614,7 +614,10 @@ __global__ __launch_bounds__(kBlock) void bucket_hook_kernel(u32* __restrict__ p
 }
 
 // The slow list (FINAL P2: edges whose source was not in C) against C | N: both ends in it -> already connected to
-// g; one end -> the other hooked under g; neither -> united.
+// g; one end -> the other hooked under g; neither -> united. Block b takes part b % kSlowSplit of P2 block
+// (b / kSlowSplit)'s region, only up to that region's count (a grid-stride over every region's capacity read the
+// count for each of C4's 134M slots, most of them empty).
+constexpr u32 kSlowSplit = 8;
 __global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ parent, const u64* __restrict__ slow,
                                                              u32 slow_cap, const Meta* __restrict__ m, u32 nblocks,
                                                              const u32* __restrict__ bits, const u32* __restrict__ giant,
@@ -622,11 +625,12 @@ __global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ p
     trace_start(kTrBkSlow);
     const u32 g = *giant;
     NoCount c;
-    const u64 total = (u64)nblocks * slow_cap;
-    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < total; i += (u64)gridDim.x * kBlock) {
-        const u32 r = (u32)(i / slow_cap), k = (u32)(i - (u64)r * slow_cap);
-        if (k >= m->slow_cnt[r]) continue;
-        const u64 e = slow[i];
+    const u32 r = blockIdx.x / kSlowSplit, part = blockIdx.x % kSlowSplit;
+    if (r >= nblocks) return;
+    const u32 cnt = m->slow_cnt[r];
+    const u64* list = slow + (u64)r * slow_cap;
+    for (u32 k = part * kBlock + threadIdx.x; k < cnt; k += kSlowSplit * kBlock) {
+        const u64 e = list[k];
         const u32 a = (u32)e, b = (u32)(e >> 32);
         if (a >= cap || b >= cap) {
             flag_err(err, kErrSlow);

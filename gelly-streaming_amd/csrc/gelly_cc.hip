@@ -1412,6 +1412,15 @@ static void mark_mutated(gcc_forest* h, bool recorded = false) {
 // start/stop events, which the runtime records from the dispatch itself: the logged duration is the kernel's
 // own execution, and no extra packets (hipEventRecord markers cost ~4 us each between dependent kernels) are
 // put between the pipeline's launches.
+// GELLY_BUCKET_STATS=1 (diagnostics): after each bucketed fold, print its lists' fill to stderr (synchronises).
+static bool bucket_stats() {
+    static const bool on = [] {
+        const char* e = std::getenv("GELLY_BUCKET_STATS");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
 // GELLY_SYNC_EACH=1 (diagnostics): synchronise after every launch, so that an asynchronous fault names its kernel.
 static bool sync_each_launch() {
     static const bool on = [] {
@@ -1815,8 +1824,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         rc = launch_k(h, "bucket_hook", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
                       h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
     if (!rc)
-        rc = launch_k(h, "bucket_slow", 0, bk::bucket_slow_kernel, dim3(grid_for((u64)p2_blocks * slow_cap, kMaxGrid)),
-                      dim3(kBlock), 0, h->d_parent, (const u64*)h->d_slow, slow_cap, (const bk::Meta*)h->d_meta, p2_blocks,
+        rc = launch_k(h, "bucket_slow", 0, bk::bucket_slow_kernel, dim3(p2_blocks * bk::kSlowSplit), dim3(kBlock), 0, h->d_parent, (const u64*)h->d_slow, slow_cap, (const bk::Meta*)h->d_meta, p2_blocks,
                       (const u32*)bits, (const u32*)giant, h->cap, h->d_err);
     if (!rc)
         rc = launch_k(h, "bucket_rest", 0, bk::bucket_rest_kernel, dim3(grid_for(n / 64 + 1, kMaxGrid)), dim3(kBlock), 0,
@@ -1825,6 +1833,21 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (rc) return rc;
     h->pending_reset = false;
     h->has_giant = true;
+    if (bucket_stats()) {  // diagnostics: the lists' fill (synchronises)
+        bk::Meta hm;
+        HIP_TRY(hipMemcpyAsync(&hm, h->d_meta, sizeof(hm), hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        u64 bk_used = 0, vl_used = 0, slow = 0;
+        for (u32 s = 0; s < ns; ++s) {
+            bk_used += std::min(hm.bk_cur[s], hm.bk_cap[s]);
+            vl_used += std::min(hm.vl_cur[s], hm.vl_cap[s]);
+        }
+        for (u32 b = 0; b < p2_blocks; ++b) slow += hm.slow_cnt[b];
+        std::fprintf(stderr, "[bucket] n=%llu ns=%u bucket entries %llu, v-list entries %llu (%.1f %%), slow %llu "
+                     "(%.1f %%), overflow %u, spill %u, g=%u\n", (unsigned long long)n, ns,
+                     (unsigned long long)bk_used, (unsigned long long)vl_used, 100.0 * vl_used / n,
+                     (unsigned long long)slow, 100.0 * slow / n, hm.ovf_cur, hm.spill, hm.gmin);
+    }
     return GCC_OK;
 }
 
