@@ -32,6 +32,7 @@ constexpr u32 kP1Tile = kP1Block * kP1Per;      // the smallest tile (bucket_app
 constexpr int kP2Block = 1024;
 constexpr int kP2Per = 8;                       // edges per thread per round (4 x 16 B)
 constexpr u32 kP2Round = kP2Block * kP2Per;     // 8192 edges per round -> at most 8192 v's per LDS tile
+constexpr u32 kP2Tile = kP2Round + 3 * 256;     // + up to 3 padding slots per slice (kMaxSlicesLds)
 constexpr u32 kMaxSlicesLds = 256;              // LDS per-slice state: id ranges up to 2^27 (larger: the old path)
 constexpr int kP3Block = 1024;
 constexpr u32 kMaxP2Blocks = 1024;
@@ -53,6 +54,7 @@ struct Meta {
 };
 
 __device__ __forceinline__ u32 lds_bit(const u32* s, u32 x) { return (s[x >> 5] >> (x & 31)) & 1u; }
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 
 // Internal consistency checks: every id a kernel takes from an internal list (buckets, slow and overflow lists) and
 // uses to index GLOBAL memory must be < cap. It always is; if one were not, the entry is skipped (never
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
     // the tile in bucket order: dynamic LDS (P1B * P1P u64, 64 / 128 KiB), set up like every kernel's LDS beyond
     // 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-slice state below is static
     extern __shared__ __attribute__((aligned(16))) u64 s_srt[];
-    __shared__ u32 s_cnt[kMaxSlicesLds], s_start[kMaxSlicesLds], s_cap[kMaxSlicesLds];
+    __shared__ u32 s_cnt[kMaxSlicesLds], s_pc[kMaxSlicesLds], s_start[kMaxSlicesLds], s_cap[kMaxSlicesLds];
     __shared__ u32 s_cpos[kMaxSlicesLds], s_cend[kMaxSlicesLds], s_p1[kMaxSlicesLds], s_l1[kMaxSlicesLds],
         s_p2[kMaxSlicesLds], s_l2[kMaxSlicesLds];
     __shared__ u64 s_base[kMaxSlicesLds];
@@ -273,26 +275,33 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
             if (ok[k]) ok[k] = edge_ok(ua[k], va[k], cap, err);
             if (ok[k]) rk[k] = atomicAdd(&s_cnt[ua[k] >> kSliceBits], 1u);
         }
+        __syncthreads();  // the tile's counts are complete
+        // every bucket's run is padded to an even length with one ~0 entry (P2 skips it), so that runs, tile
+        // slots and list positions stay even and the write-out moves a pair of edges per 16-B store
+        for (u32 s = threadIdx.x; s < ns; s += P1B) s_pc[s] = (s_cnt[s] + 1) & ~1u;
         __syncthreads();
-        count_scan<P1B>(s_cnt, s_start, ns, s_wsum);
-        for (u32 s = threadIdx.x; s < ns; s += P1B)
-            if (s_cnt[s]) reserve_run(runs, s, s_cnt[s], &m->bk_cur[s], s_cap[s]);
+        count_scan<P1B>(s_pc, s_start, ns, s_wsum);
+        for (u32 s = threadIdx.x; s < ns; s += P1B) {
+            if (s_pc[s]) reserve_run(runs, s, s_pc[s], &m->bk_cur[s], s_cap[s]);
+            if (s_cnt[s] & 1) s_srt[s_start[s] + s_cnt[s]] = ~0ull;
+        }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < P1P; ++k)
             if (ok[k]) s_srt[s_start[ua[k] >> kSliceBits] + rk[k]] = ((u64)va[k] << 32) | ua[k];
         __syncthreads();
-        const u32 tot = s_start[ns - 1] + s_cnt[ns - 1];
-        for (u32 x = threadIdx.x; x < tot; x += P1B) {
-            const u64 e = s_srt[x];
-            const u32 s = (u32)e >> kSliceBits;
-            const u32 off = run_pos(runs, s, x - s_start[s]);
+        const u32 tot2 = (s_start[ns - 1] + s_pc[ns - 1]) / 2;
+        for (u32 x2 = threadIdx.x; x2 < tot2; x2 += P1B) {
+            const u64x2 e = reinterpret_cast<const u64x2*>(s_srt)[x2];  // slot 2 x2 is never padding
+            const u32 s = (u32)e.x >> kSliceBits;
+            const u32 off = run_pos(runs, s, 2 * x2 - s_start[s]);     // even: both slots in one chunk
             if (off != 0xFFFFFFFFu) {
-                bk[s_base[s] + off] = e;
+                *reinterpret_cast<u64x2*>(bk + s_base[s] + off) = e;   // 16-B aligned (bases: 16-entry multiples)
             } else {  // the bucket is full (its estimate was low): the overflow list (folded at the end)
-                const u32 o = atomicAdd(&m->ovf_cur, 1u);
-                if (o < ovf_cap) ovf[o] = e;
-                else m->spill = 1u;  // -> bucket_rest_kernel folds the whole batch again (exact, slow)
+                const u32 o = atomicAdd(&m->ovf_cur, e.y != ~0ull ? 2u : 1u);
+                if (o < ovf_cap) ovf[o] = e.x;
+                if (e.y != ~0ull && o + 1 < ovf_cap) ovf[o + 1] = e.y;
+                if (o + (e.y != ~0ull ? 1u : 0u) >= ovf_cap) m->spill = 1u;  // -> bucket_rest: the whole batch again
             }
         }
         __syncthreads();
@@ -350,9 +359,10 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     trace_start(FINAL ? kTrBkP2 : kTrBkP2Seed);
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     u32* s_bits = s_dyn;                                   // kSliceWords
-    u32* s_vt = s_dyn + kSliceWords;                       // kP2Round
-    u32* s_cnt2 = s_vt + kP2Round;                         // 2 x kMaxSlicesLds (double-buffered)
-    u32* s_start = s_cnt2 + 2 * kMaxSlicesLds;             // kMaxSlicesLds
+    u32* s_vt = s_dyn + kSliceWords;                       // kP2Tile: the round's targets + run padding
+    u32* s_cnt2 = s_vt + kP2Tile;                          // 2 x kMaxSlicesLds (double-buffered)
+    u32* s_pc = s_cnt2 + 2 * kMaxSlicesLds;                // kMaxSlicesLds: counts padded to 4
+    u32* s_start = s_pc + kMaxSlicesLds;                   // kMaxSlicesLds
     u32* s_vcap = s_start + kMaxSlicesLds;                 // kMaxSlicesLds
     u32* s_run = s_vcap + kMaxSlicesLds;                   // 6 x kMaxSlicesLds: the chunk state (Runs)
     u64* s_vbase = reinterpret_cast<u64*>(s_run + 6 * kMaxSlicesLds);   // kMaxSlicesLds
@@ -465,9 +475,13 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 }
             }
             __syncthreads();  // (1) counts of this round complete
-            count_scan<kP2Block>(s_cnt, s_start, ns, s_wsum);
+            // runs padded to a multiple of 4 with UNSEEN (P3 skips it): a lane writes 4 targets per 16-B store
+            for (u32 s = threadIdx.x; s < ns; s += kP2Block) s_pc[s] = (s_cnt[s] + 3) & ~3u;
+            __syncthreads();
+            count_scan<kP2Block>(s_pc, s_start, ns, s_wsum);
             for (u32 s = threadIdx.x; s < ns; s += kP2Block) {
-                if (s_cnt[s]) reserve_run(runs, s, s_cnt[s], &m->vl_cur[s], s_vcap[s]);
+                if (s_pc[s]) reserve_run(runs, s, s_pc[s], &m->vl_cur[s], s_vcap[s]);
+                for (u32 j = s_cnt[s]; j < s_pc[s]; ++j) s_vt[s_start[s] + j] = 0xFFFFFFFFu;
                 s_cnt2[(rb ^ 1) * kMaxSlicesLds + s] = 0;  // the next round's buffer
             }
             __syncthreads();  // (2) starts + reservations
@@ -475,13 +489,19 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             for (int k = 0; k < kP2Per; ++k)
                 if (emit[k]) s_vt[s_start[va[k] >> kSliceBits] + rk[k]] = va[k];
             __syncthreads();  // (3) tile in bucket order
-            const u32 tot = s_start[ns - 1] + s_cnt[ns - 1];
-            for (u32 x = threadIdx.x; x < tot; x += kP2Block) {
-                const u32 v = s_vt[x];
-                const u32 s = v >> kSliceBits;
-                const u32 off = run_pos(runs, s, x - s_start[s]);
-                if (off != 0xFFFFFFFFu) vl[s_vbase[s] + off] = v;
-                else if (FINAL) hook_g(parent, g, v);  // the v-list is full: (u in C, v) = union(g, v) now
+            const u32 tot4 = (s_start[ns - 1] + s_pc[ns - 1]) / 4;
+            for (u32 x4 = threadIdx.x; x4 < tot4; x4 += kP2Block) {
+                const u4 v = reinterpret_cast<const u4*>(s_vt)[x4];  // slot 4 x4 is never padding
+                const u32 s = v.x >> kSliceBits;
+                const u32 off = run_pos(runs, s, 4 * x4 - s_start[s]);  // a multiple of 4: one chunk
+                if (off != 0xFFFFFFFFu) {
+                    *reinterpret_cast<u4*>(vl + s_vbase[s] + off) = v;  // 16-B aligned (bases: 16-entry multiples)
+                } else if (FINAL) {  // the v-list is full: (u in C, v) = union(g, v) now
+                    hook_g(parent, g, v.x);
+                    if (v.y != 0xFFFFFFFFu) hook_g(parent, g, v.y);
+                    if (v.z != 0xFFFFFFFFu) hook_g(parent, g, v.z);
+                    if (v.w != 0xFFFFFFFFu) hook_g(parent, g, v.w);
+                }
             }
             rb ^= 1;  // the write-out above is done before anyone passes the next round's barrier (1)
         }

@@ -1190,7 +1190,7 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
 #include "bucket_fold.h"
 
 static constexpr size_t slice_filter_lds() {  // bucket_fold.h slice_filter_kernel's dynamic LDS
-    return (bk::kSliceWords + bk::kP2Round + 10 * bk::kMaxSlicesLds) * sizeof(u32) + bk::kMaxSlicesLds * sizeof(u64) +
+    return (bk::kSliceWords + bk::kP2Tile + 11 * bk::kMaxSlicesLds) * sizeof(u32) + bk::kMaxSlicesLds * sizeof(u64) +
            (bk::kP2Block / 64) * kRing * sizeof(u64);
 }
 
