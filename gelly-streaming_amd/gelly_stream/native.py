@@ -21,7 +21,7 @@ GCC_GEN_RMAT = 2
 GCC_GEN_GNM = 3
 GCC_GEN_ADVERSARIAL = 4
 
-ERRORS = {-1: "GCC_E_INVALID", -2: "GCC_E_HIP", -3: "GCC_E_NODEV", -4: "GCC_E_OOM"}
+ERRORS = {-1: "GCC_E_INVALID", -2: "GCC_E_HIP", -3: "GCC_E_NODEV", -4: "GCC_E_OOM", -5: "GCC_E_INTERNAL"}
 
 
 class GellyCCError(RuntimeError):

@@ -76,3 +76,15 @@ def test_null_handle_is_an_error_not_a_crash():
     rc = native.lib().gcc_forest_size(None, None)
     assert rc == -1
     assert native.lib().gcc_forest_destroy(None) == 0
+
+
+def test_every_error_code_is_named():
+    """Each GCC_E_* code the header defines has its name in the Python binding's ERRORS table."""
+    import re
+
+    from gelly_stream import native
+
+    text = open(os.path.join(ROOT, "include", "gelly_cc.h")).read()
+    codes = {int(v): k for k, v in re.findall(r"#define (GCC_E_\w+) \((-\d+)\)", text)}
+    assert codes, "no error codes found in the header"
+    assert {c: native.ERRORS.get(c) for c in codes} == codes
