@@ -510,7 +510,7 @@ __global__ __launch_bounds__(1024) void giant_vote_kernel(u32* __restrict__ pare
 // lanes' 4-bit nibbles are OR-ed into the chunk's 4 bitmap words. labels == nullptr: a mid-fold refresh of the
 // bitmap alone (refresh_now); bits == nullptr (the filter off): the labels alone. Prefetched parent values are historically valid (splitting stores only write
 // ancestors), so a find from one is exact.
-constexpr int kBitsU = 4;
+constexpr int kBitsU = 1;  // chunks per wave per batch (A/B: 1 beat 2, 4, 8 on C2 x 16)
 __device__ __forceinline__ void chunk_bits(u64* bits, u64 nwords, u64 ch, u32 lane, u32 g, const u32 (&lab)[4]) {
     u64 w = 0;
     if (g != UNSEEN)
@@ -602,7 +602,7 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
 // bloom in LDS; a lane reads 4 consecutive ids (16 B) and a wave covers 256 ids = 4 bitmap words of the
 // tracked component (as compress_bits_kernel). The block also clears its share of the other bloom buffer.
 constexpr int kIncBlock = 1024;
-constexpr int kIncU = 4;  // 256-id chunks per wave in flight
+constexpr int kIncU = 2;  // 256-id chunks per wave per batch (A/B: 2 beat 1, 4 and 8 on C5; profiles/r2_ab_chunk_batches.log)
 using gcc::inc_label;  // uf_device.h: shared with the host replay
 
 // INPLACE: labels == parent. parent[] is already canonical except where a marked parent needs the find, so only
