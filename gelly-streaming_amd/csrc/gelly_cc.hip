@@ -1266,6 +1266,9 @@ struct FoldTune {
     u64 seed_div1 = 3;  // the first BFS pass covers 1/seed_div1 of the batch (>= 1/seed_div)
     double seed_refresh = 0;  // refresh point of a seeded batch (fraction; 0 = none)
     bool hook = true;  // direct atomicMin hook of (T, new id) edges in the filtered stream (filter_round)
+    // the filtered fold copies the bitmap into every CU's LDS only when the batch has at least lds_edges_per_word
+    // edges per bitmap word (u64); a shorter batch looks its endpoints up in the global (L2-resident) bitmap
+    double lds_edges_per_word = 0.0;
     u32 drain_at = 64;  // a wave drains its slow-edge ring once this many edges are pending (1..64)
     bool seed_nt = true;  // non-temporal loads in the BFS passes (false: the prefix may stay in the MALL)
     bool seed_global = false;  // also seed when the bitmap does not fit LDS (global-bitmap BFS lookups)
@@ -1584,7 +1587,7 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (n == 0) return GCC_OK;
     h->rec_all = false;  // the filtered fold does not record its mutations
     const u32 nw = h->nwords() + (h->nwords() & 1);  // u64 bitmap words, rounded to 16 B
-    const bool lds = nw <= kLdsBitmapMaxWords;
+    const bool lds = nw <= kLdsBitmapMaxWords && (double)n >= h->tune.lds_edges_per_word * (double)nw;
     const u32 nblocks = lds ? (u32)h->n_cu : kMaxGrid;
     if (!h->d_qcount) HIP_TRY(hipMalloc((void**)&h->d_qcount, kMaxGrid * sizeof(u32)));
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
@@ -2804,6 +2807,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "depth") t.depth = (int)value == 8 ? 8 : 4;
     else if (k == "seed") t.seed = value != 0;
     else if (k == "hook") t.hook = value != 0;
+    else if (k == "lds_edges_per_word") t.lds_edges_per_word = std::max(0.0, value);
     else if (k == "drain_at") t.drain_at = (u32)std::max(1.0, std::min(64.0, value));
     else if (k == "seed_nt") t.seed_nt = value != 0;
     else if (k == "seed_global") t.seed_global = value != 0;
