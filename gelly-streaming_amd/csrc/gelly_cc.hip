@@ -1785,6 +1785,9 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u32 ovf_cap = (u32)std::min<u64>(h->ovf_cap, 0xFFFFFFF0ull);
     const u32 items = 4 * (u32)h->n_cu;  // dequeue items per P2 / P3 launch (parts of the slices)
     const u32 cps = std::max<u32>(1, (items + ns - 1) / ns);
+    // A block loads a part's 64 KiB bitmap slice into LDS per item: a pass over few edges (the seeding levels of a
+    // small batch) takes fewer, longer parts, about 64K edges per part at least
+    const u32 cps_seed = (u32)std::max<u64>(1, std::min<u64>(cps, (u64)((double)n * t.bucket_sample) / ((u64)ns << 16)));
     const size_t f_lds = slice_filter_lds(), h_lds = bk::kSliceWords * sizeof(u32);
     const size_t vl_cur_off = offsetof(bk::Meta, vl_cur);
     u32 slot = 0;
@@ -1807,11 +1810,11 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     for (int l = 0; l < levels && !rc; ++l) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
         rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
-                      f_lds, h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps, frac,
+                      f_lds, h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps_seed, frac,
                       slot++, h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err);
         if (!rc)
             rc = launch_k(h, "seed_hook", 0, bk::slice_hook_kernel<false>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                          bits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
+                          bits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps_seed, slot++, h->cap, h->d_err);
     }
     // parent[] := C ? g : UNSEEN (the reset), then every bucketed edge, the overflow list, a spill
     if (!rc)
