@@ -2875,7 +2875,8 @@ int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size) {
         if (in_fold && std::strcmp(k.name, "compress") != 0 && std::strcmp(k.name, "compress_inc") != 0) {  // this fold's
             if (first < 0) first = k.ev;
             last = k.ev;
-            if (!std::strcmp(k.name, "filtered") || !std::strcmp(k.name, "plain") || !std::strcmp(k.name, "sample"))
+            if (!std::strcmp(k.name, "filtered") || !std::strcmp(k.name, "plain") || !std::strcmp(k.name, "sample") ||
+                !std::strcmp(k.name, "bucket"))  // the bucketed fold's P1 passes over every edge of the batch once
                 fold_edges += k.edges;
         } else if (in_fold) {
             close_fold();
