@@ -523,6 +523,18 @@ __device__ __forceinline__ void chunk_bits(u64* bits, u64 nwords, u64 ch, u32 la
     if ((lane & 15) == 0 && wi < nwords) bits[wi] = w;
 }
 
+// The same packing for the merge message's "others" mask: seen ids outside g's component (all seen ids if no g).
+__device__ __forceinline__ void chunk_oth(u64* oth, u64 nwords, u64 ch, u32 lane, u32 g, const u32 (&lab)[4]) {
+    auto o = [&](u32 l) { return (u32)(l != UNSEEN && l != g); };
+    u64 w = (u64)(o(lab[0]) | (o(lab[1]) << 1) | (o(lab[2]) << 2) | (o(lab[3]) << 3)) << (4 * (lane & 15));
+    w |= __shfl_xor(w, 1, 64);
+    w |= __shfl_xor(w, 2, 64);
+    w |= __shfl_xor(w, 4, 64);
+    w |= __shfl_xor(w, 8, 64);
+    const u64 wi = ch * 4 + (lane >> 4);
+    if ((lane & 15) == 0 && wi < nwords) oth[wi] = w;
+}
+
 static inline unsigned chunk_grid(u64 n, int per_wave, int block, unsigned max_blocks) {  // waves for 256-id chunks
     const u64 waves = ((n + 255) / 256 + per_wave - 1) / per_wave;
     const u64 b = (waves * 64 + block - 1) / block;
@@ -532,9 +544,9 @@ static inline unsigned chunk_grid(u64 n, int per_wave, int block, unsigned max_b
 __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__ parent, u32* __restrict__ labels, u32 n,
                                                                const u32* __restrict__ giant_prev,
                                                                u32* __restrict__ giant_next, u64* __restrict__ bits,
-                                                               u32* __restrict__ bloom_clear) {
+                                                               u32* __restrict__ bloom_clear, u64* __restrict__ oth) {
     trace_start(kTrCompressBits);
-    __shared__ u32 s_g;
+    __shared__ u32 s_g, s_g0;
     NoCount c;
     const u32 lane = threadIdx.x & 63;
     const u64 nwords = ((u64)n + 63) / 64;
@@ -555,10 +567,14 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
     if (threadIdx.x == 0) {
         const u32 g0 = giant_prev ? *giant_prev : UNSEEN;
         s_g = (g0 == UNSEEN) ? UNSEEN : UF::find_from(parent, g0, parent[g0], c);
+        s_g0 = g0;
         if (blockIdx.x == 0 && giant_next) *giant_next = s_g;
     }
     __syncthreads();
     const u32 g = s_g;
+    // the tracked component's previous root g0 (now under g, or g itself): the bucketed fold and the seeding hang
+    // most of a giant's ids straight under it, so its children are labelled g without a walk
+    const u32 g0 = s_g0;
     for (u64 base = wave; base < nfull; base += (u64)kBitsU * nwaves) {
         u32x4 cur[kBitsU];
 #pragma unroll
@@ -572,15 +588,17 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
             const u32 v0 = (u32)(ch * 256 + 4 * lane);
             const u32x4 p = cur[k];
             u32 lab[4];
-            lab[0] = (p.x >= v0) ? p.x : UF::find_from(parent, v0, p.x, c);
-            lab[1] = (p.y >= v0 + 1) ? p.y : UF::find_from(parent, v0 + 1, p.y, c);
-            lab[2] = (p.z >= v0 + 2) ? p.z : UF::find_from(parent, v0 + 2, p.z, c);
-            lab[3] = (p.w >= v0 + 3) ? p.w : UF::find_from(parent, v0 + 3, p.w, c);
+            // a child of the tracked root g (a root during the compress) needs no find: most ids of a giant
+            lab[0] = (p.x >= v0 || p.x == g) ? p.x : (p.x == g0 ? g : UF::find_from(parent, v0, p.x, c));
+            lab[1] = (p.y >= v0 + 1 || p.y == g) ? p.y : (p.y == g0 ? g : UF::find_from(parent, v0 + 1, p.y, c));
+            lab[2] = (p.z >= v0 + 2 || p.z == g) ? p.z : (p.z == g0 ? g : UF::find_from(parent, v0 + 2, p.z, c));
+            lab[3] = (p.w >= v0 + 3 || p.w == g) ? p.w : (p.w == g0 ? g : UF::find_from(parent, v0 + 3, p.w, c));
             if (labels) {
                 const u32x4 o = {lab[0], lab[1], lab[2], lab[3]};
                 *reinterpret_cast<u32x4*>(labels + v0) = o;
             }
             if (bits) chunk_bits(bits, nwords, ch, lane, g, lab);
+            if (oth) chunk_oth(oth, nwords, ch, lane, g, lab);
         }
     }
     if (nfull * 256 < n && wave == nfull % nwaves) {  // the partial last chunk: id by id
@@ -592,6 +610,7 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
                 if (labels) labels[v0 + k] = lab[k];
             }
         if (bits) chunk_bits(bits, nwords, nfull, lane, g, lab);
+        if (oth) chunk_oth(oth, nwords, nfull, lane, g, lab);
     }
 }
 
@@ -994,68 +1013,186 @@ __global__ __launch_bounds__(kBlock) void seed_pack_kernel(u32* __restrict__ par
 // ------------------------------------------------------------------------------------------------
 // Cross-GPU merge message (include/gelly_cc.h: header, giant bitmap, (v, label) list of the other seen ids).
 // ------------------------------------------------------------------------------------------------
-constexpr unsigned kMsgWordsPerBlock = 64;  // 4096 ids per block; one atomicAdd per block with "others"
+constexpr unsigned kMsgWordsPerBlock = 256;  // 16K ids per count block: 16 waves x 16 words
+constexpr int kMsgBlock = 1024;
 
-// Encode from canonical labels. Each block owns kMsgWordsPerBlock consecutive 64-id words: pass 1 counts its
-// "others" (4 words in flight per wave), one atomicAdd reserves its slice of the list, pass 2 writes the bitmap
-// words and the pairs (the block's 16 KiB of labels are re-read from L2). msg_header_kernel runs first.
-__global__ __launch_bounds__(kBlock) void msg_encode_kernel(const u32* __restrict__ labels, u32 n, u32* __restrict__ hdr,
-                                                            u64* __restrict__ bits, u32* __restrict__ others, u64 cap) {
-    __shared__ u32 s_cnt[kBlock / 64];
-    __shared__ u32 s_base;
-    constexpr int kW = kMsgWordsPerBlock / (kBlock / 64);  // words per wave
+// The label of v from a forest that may not be compressed: FIND follows parent pointers with read-only loads
+// (no path splitting: a find of the encode and the same id's find in msg_write_kernel must agree, and nothing
+// mutates parent[] between them), otherwise parent[] already holds the canonical labels. g is the tracked
+// component's current root and g0 its root at the last refresh (now under g, or g itself): their children are
+// labelled without a walk.
+template <bool FIND>
+__device__ __forceinline__ u32 msg_label(const u32* __restrict__ parent, u32 v, u32 p, u32 g, u32 g0) {
+    if (!FIND || p >= v || p == g) return p;  // a label, a root or UNSEEN
+    if (p == g0) return g;
+    NoCount c;
+    return UFRead::find_from(const_cast<u32*>(parent), v, p, c);
+}
+
+// Encode, pass 1 of 3: each block owns kMsgWordsPerBlock consecutive 64-id words (16 per wave). It writes the
+// giant bitmap words (into the message and, with `mine`, into the forest's own tracked-component bitmap), the
+// mask of every word's "other" seen ids (scratch, 8 B per word) and its count of others. No atomics: round 1's
+// single kernel reserved list space with one atomicAdd per 4096-id block on one header word, and 16K
+// same-address atomics serialised at the memory side (476 us of a 64M-id encode, tools/merge_probe.py).
+template <bool FIND>
+__global__ __launch_bounds__(kMsgBlock) void msg_count_kernel(const u32* __restrict__ parent, u32 n,
+                                                              const u32* __restrict__ hdr, const u32* __restrict__ giant_prev,
+                                                              u64* __restrict__ bits, u64* __restrict__ mine,
+                                                              u64* __restrict__ oth, u32* __restrict__ cnt) {
+    __shared__ u32 s_cnt[kMsgBlock / 64];
+    constexpr int kW = kMsgWordsPerBlock / (kMsgBlock / 64);  // words per wave
     const u32 g = hdr[0];
+    const u32 g0 = giant_prev ? *giant_prev : UNSEEN;
     const u64 nw = ((u64)n + 63) / 64;
     const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const u64 w0 = (u64)blockIdx.x * kMsgWordsPerBlock + (u64)wave * kW;
     u32 l[kW];
 #pragma unroll
-    for (int k = 0; k < kW; ++k) {
+    for (int k = 0; k < kW; ++k) {  // all loads of the wave in flight before any find
         const u64 v = (w0 + k) * 64 + lane;
-        l[k] = (w0 + k < nw && v < n) ? labels[v] : UNSEEN;
+        l[k] = (w0 + k < nw && v < n) ? parent[v] : UNSEEN;
     }
-    u32 cnt = 0;
-#pragma unroll
-    for (int k = 0; k < kW; ++k) cnt += (u32)__popcll(__ballot(l[k] != UNSEEN && l[k] != g));
-    if (lane == 0) s_cnt[wave] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        u32 tot = 0;
-        for (int k = 0; k < kBlock / 64; ++k) {
-            const u32 c = s_cnt[k];
-            s_cnt[k] = tot;  // exclusive prefix over the block's waves
-            tot += c;
-        }
-        s_base = tot ? atomicAdd(&hdr[1], tot) : 0;  // hdr[1] ends as the true count
-    }
-    __syncthreads();
-    u64 pos = (u64)s_base + s_cnt[wave];
+    u32 total = 0;
 #pragma unroll
     for (int k = 0; k < kW; ++k) {
         const u64 w = w0 + k;
-        const unsigned long long in_g = __ballot(l[k] != UNSEEN && l[k] == g);
-        const unsigned long long oth = __ballot(l[k] != UNSEEN && l[k] != g);
-        if (lane == 0 && w < nw) bits[w] = in_g;
-        if ((oth >> lane) & 1ull) {
-            const u64 q = pos + (u64)__popcll(oth & ((1ull << lane) - 1ull));
-            if (q < cap) {
-                others[2 * q] = (u32)(w * 64 + lane);
-                others[2 * q + 1] = l[k];
-            }
+        const u32 lab = msg_label<FIND>(parent, (u32)(w * 64 + lane), l[k], g, g0);
+        const unsigned long long in_g = __ballot(lab != UNSEEN && lab == g);
+        const unsigned long long o = __ballot(lab != UNSEEN && lab != g);
+        if (lane == 0 && w < nw) {
+            bits[w] = in_g;
+            if (mine) mine[w] = in_g;
+            oth[w] = o;
         }
-        pos += (u64)__popcll(oth);
+        total += (u32)__popcll(o);
+    }
+    if (lane == 0) s_cnt[wave] = total;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u32 t = 0;
+        for (int k = 0; k < kMsgBlock / 64; ++k) t += s_cnt[k];
+        cnt[blockIdx.x] = t;
+    }
+}
+
+// Encode, pass 1 after a compress that wrote the masks (compress_bits_kernel's chunk_oth): per count block the
+// number of other seen ids, read from the 8-B masks instead of the 4-B labels, and the forest's giant bitmap
+// copied into the message. One word per thread.
+__global__ __launch_bounds__(kBlock) void msg_cnt_kernel(const u64* __restrict__ oth, const u64* __restrict__ mine,
+                                                         u64* __restrict__ bits, u64 nw, u32* __restrict__ cnt) {
+    static_assert(kMsgWordsPerBlock == kBlock, "one word per thread");
+    __shared__ u32 s_tot[kBlock / 64];
+    const u64 w = (u64)blockIdx.x * kMsgWordsPerBlock + threadIdx.x;
+    u32 c = 0;
+    if (w < nw) {
+        c = (u32)__popcll(oth[w]);
+        bits[w] = mine[w];
+    }
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0) s_tot[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u32 t = 0;
+        for (int k = 0; k < kBlock / 64; ++k) t += s_tot[k];
+        cnt[blockIdx.x] = t;
+    }
+}
+
+// Encode, pass 2: one block, the exclusive prefix of the count blocks' totals -> base[]; hdr[1] = the list's
+// true length (a receiver compares it with the capacity: a longer list means a repair round).
+constexpr int kScanBlock = 1024;
+constexpr int kScanPer = 4;  // items per thread and round: 4096 count blocks (C4's 64M ids) in one round
+__global__ __launch_bounds__(kScanBlock) void msg_scan_kernel(const u32* __restrict__ cnt, u32 nb, u32* __restrict__ base,
+                                                              u32* __restrict__ hdr) {
+    __shared__ u64 s_wave[kScanBlock / 64];
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u64 carry = 0;
+    for (u32 r0 = 0; r0 < nb; r0 += kScanBlock * kScanPer) {
+        const u32 b0 = r0 + threadIdx.x * kScanPer;
+        u32 x[kScanPer];
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) x[k] = (b0 + k < nb) ? cnt[b0 + k] : 0;  // all in flight
+        u64 t = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) t += x[k];
+        u64 incl = t;  // wave inclusive scan of the threads' sums
+        for (int off = 1; off < 64; off <<= 1) {
+            const u64 y = __shfl_up(incl, off, 64);
+            if (lane >= (u32)off) incl += y;
+        }
+        if (lane == 63) s_wave[wave] = incl;
+        __syncthreads();
+        u64 before = carry, total = carry;
+        for (u32 k = 0; k < kScanBlock / 64; ++k) {
+            if (k < wave) before += s_wave[k];
+            total += s_wave[k];
+        }
+        u64 run = before + incl - t;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            if (b0 + k < nb) base[b0 + k] = (u32)min<u64>(run, 0xFFFFFFFFull);
+            run += x[k];
+        }
+        carry = total;
+        __syncthreads();  // s_wave is rewritten by the next round
+    }
+    if (threadIdx.x == 0) hdr[1] = (u32)min<u64>(carry, 0xFFFFFFFFull);
+}
+
+// Encode, pass 3: one 256-thread block per count block, one word per lane. The masks locate the other seen ids
+// (sparse: 0.2 % of C4's ids at an 8-way split), wave and block prefixes of their counts place them, and only
+// those ids are read again. Pairs come out in id order, so a message (and a serialized summary) is deterministic.
+template <bool FIND>
+__global__ __launch_bounds__(kBlock) void msg_write_kernel(const u32* __restrict__ parent, u32 n, const u64* __restrict__ oth,
+                                                           const u32* __restrict__ base, const u32* __restrict__ hdr,
+                                                           const u32* __restrict__ giant_prev, u32* __restrict__ others,
+                                                           u64 cap) {
+    static_assert(kMsgWordsPerBlock == kBlock, "one word per lane");
+    __shared__ u32 s_tot[kBlock / 64];
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const u64 nw = ((u64)n + 63) / 64;
+    const u64 w = (u64)blockIdx.x * kMsgWordsPerBlock + threadIdx.x;
+    u64 m = w < nw ? oth[w] : 0;
+    const u32 c = (u32)__popcll(m);
+    u32 incl = c;
+    for (int off = 1; off < 64; off <<= 1) {
+        const u32 x = __shfl_up(incl, off, 64);
+        if (lane >= (u32)off) incl += x;
+    }
+    if (lane == 63) s_tot[wave] = incl;
+    __syncthreads();
+    u64 pos = (u64)base[blockIdx.x] + (incl - c);
+    for (u32 k = 0; k < wave; ++k) pos += s_tot[k];
+    if (!m) return;
+    const u32 g = hdr[0];
+    const u32 g0 = giant_prev ? *giant_prev : UNSEEN;
+    while (m) {
+        const u32 v = (u32)(w * 64 + (u64)__builtin_ctzll(m));
+        m &= m - 1;
+        if (pos < cap) {
+            others[2 * pos] = v;
+            others[2 * pos + 1] = msg_label<FIND>(parent, v, parent[v], g, g0);
+        }
+        ++pos;
     }
 }
 
 // One wave: the header, and the witness slots of the absorb that follows a merge's all_gather re-armed to UNSEEN
-// (saves that absorb a memset launch).
+// (saves that absorb a memset launch). With `parent` (an uncompressed forest) the tracked root is followed to the
+// component's current root, which is also stored in giant_next (the forest's next tracked-root slot).
 __global__ void msg_header_kernel(u32* __restrict__ hdr, const u32* __restrict__ giant_root, u32 has_giant, u32 n,
-                                  u32* __restrict__ witness) {
+                                  u32* __restrict__ witness, const u32* __restrict__ parent, u32* __restrict__ giant_next) {
     if (threadIdx.x == 0) {
-        hdr[0] = has_giant ? *giant_root : UNSEEN;
+        u32 g = has_giant ? *giant_root : UNSEEN;
+        if (parent && g < n) {
+            NoCount c;
+            g = UFRead::find_from(const_cast<u32*>(parent), g, parent[g], c);
+        }
+        hdr[0] = g;
         hdr[1] = 0;
         hdr[2] = n;
         hdr[3] = 0;
+        if (giant_next) *giant_next = g;
     }
     if (witness) witness[threadIdx.x] = UNSEEN;
 }
@@ -1120,7 +1257,8 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict
                                                                  u64 stride, u32 count, u32 skip, u32 n,
                                                                  const u64* __restrict__ mine,
                                                                  const u32* __restrict__ tracked,
-                                                                 const u32* __restrict__ witness) {
+                                                                 const u32* __restrict__ witness,
+                                                                 const u64* __restrict__ seen_oth) {
     __shared__ u32 s_g[kMaxPeers];
     __shared__ u32 s_w[kMaxPeers];
     msg_peers(msgs, stride, count, skip, n, true, witness, s_g, s_w);
@@ -1129,16 +1267,60 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict
     const u64 nw = ((u64)n + 63) / 64;
     const u64 wave = (u64)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const u64 waves = (u64)gridDim.x * (kBlock / 64);
-    for (u64 w = wave; w < nw; w += waves) {
-        // lane p < count loads peer p's word; the overlapping peers' words are OR-ed across the wave
-        u64 m = 0;
-        if (lane < count && s_g[lane] != UNSEEN && s_w[lane] != UNSEEN)
-            m = reinterpret_cast<const u64*>(msgs + lane * stride + GCC_MSG_HEADER_BYTES)[w];
-        for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off, 64);
-        if (!m) continue;
-        const u64 todo = m & ~mine[w];
-        const u32 v = (u32)(w * 64 + lane);
-        if (((todo >> lane) & 1ull) && v != R) gcc::absorb_join(parent, v, R);  // a new id: one plain store
+    // 64 words per wave and round, one per lane: the overlapping peers' words and T's word of every lane in flight
+    // at once (coalesced: consecutive words across the lanes), then the new ids word by word, one id per lane, four
+    // words' parent loads in flight before their stores. (Round 1 took one word per wave and round: its peer
+    // loads, OR-shuffles, T load and stores were one dependent chain per 64 ids, 284 us on C4's 64M ids.)
+    for (u64 w0 = wave * 64; w0 < nw; w0 += waves * 64) {
+        const u64 w = w0 + lane;
+        u64 m = 0, so = ~0ull;
+        if (w < nw) {
+            for (u32 p = 0; p < count; ++p)
+                if (s_g[p] != UNSEEN && s_w[p] != UNSEEN)
+                    m |= reinterpret_cast<const u64*>(msgs + p * stride + GCC_MSG_HEADER_BYTES)[w];
+            if (m) m &= ~mine[w];
+            if (m && seen_oth) so = seen_oth[w];
+        }
+        unsigned long long todo_words = __ballot(m != 0);
+        if (seen_oth) {  // the encode's masks say which ids outside T are seen: the others are new, no load needed
+            while (todo_words) {
+                const int j = __builtin_ctzll(todo_words);
+                todo_words &= todo_words - 1;
+                const u64 t = __shfl(m, j, 64);
+                const u64 sj = __shfl(so, j, 64);
+                const u32 v = (u32)((w0 + (u64)j) * 64 + lane);
+                if (((t >> lane) & 1ull) && v != R) {
+                    if (v > R && !((sj >> lane) & 1ull)) gcc::st(&parent[v], R);  // a new id: one plain store
+                    else gcc::absorb_join(parent, v, R);
+                }
+            }
+            continue;
+        }
+        while (todo_words) {
+            constexpr int kU = 4;
+            u32 v[kU];
+            bool on[kU];
+            u32 pv[kU];
+#pragma unroll
+            for (int k = 0; k < kU; ++k) {
+                on[k] = false;
+                v[k] = 0;
+                if (todo_words) {
+                    const int j = __builtin_ctzll(todo_words);
+                    todo_words &= todo_words - 1;
+                    const u64 t = __shfl(m, j, 64);
+                    v[k] = (u32)((w0 + (u64)j) * 64 + lane);
+                    on[k] = ((t >> lane) & 1ull) && v[k] != R;
+                }
+                pv[k] = on[k] ? gcc::ld(&parent[v[k]]) : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < kU; ++k)
+                if (on[k]) {
+                    if (v[k] > R && pv[k] == UNSEEN) gcc::st(&parent[v[k]], R);  // a new id: one plain store
+                    else gcc::absorb_join(parent, v[k], R);
+                }
+        }
     }
 }
 
@@ -1339,6 +1521,9 @@ struct gcc_forest {
     // scratch for cross-device merges
     u32* d_scratch = nullptr;
     u32* d_witness = nullptr;  // absorb_many: per-peer id shared with the tracked component
+    u64* d_msg_oth = nullptr;  // encode scratch (gcc_forest_encode): per word, the seen ids outside the tracked component
+    u64 version = 0;      // bumped by every mutation of parent[] (with host_valid = false)
+    u64 enc_version = ~0ull;  // `version` when d_msg_oth was written: equal = the masks still describe parent[]
     bool witness_armed = false;  // the last encode already reset d_witness (stream-ordered before the next absorb)
 
     unsigned long long* d_counts = nullptr;
@@ -1407,6 +1592,7 @@ int gcc_check_device(int device) {
 // incremental compress until the next full one
 static void mark_mutated(gcc_forest* h, bool recorded = false) {
     h->host_valid = false;
+    ++h->version;
     h->compressed = false;
     if (!recorded) h->rec_all = false;
 }
@@ -1506,13 +1692,16 @@ static bool inc_forest(const gcc_forest* h) {
 
 // compress into the spare buffer and swap; with the filter on, refresh the giant bitmap from the new labels.
 // Incremental (compress_inc_kernel) when every mutation since the last compress was recorded.
-static int compress_now(gcc_forest* h, const char* name = "compress") {
+// oth (the merge encode): a full compress also writes the others mask of every 64-id word (chunk_oth); returns
+// whether it did (only the full compress of a filtered forest can).
+static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth = nullptr, bool* oth_done = nullptr) {
     int rc = GCC_OK;
     bool inplace = false;  // the compress rewrote d_parent itself (no swap)
-    const bool inc_here = inc_forest(h);
+    const bool inc_here = inc_forest(h) && !oth;  // the encode wants the masks: a full compress
     if (!h->filter_enabled()) {
         rc = launch_k(h, name, 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)), dim3(kBlock), 0,
-                      h->d_parent, h->d_spare, h->cap, (const u32*)nullptr, (u32*)nullptr, (u64*)nullptr, (u32*)nullptr);
+                      h->d_parent, h->d_spare, h->cap, (const u32*)nullptr, (u32*)nullptr, (u64*)nullptr, (u32*)nullptr,
+                      (u64*)nullptr);
     } else {
         rc = alloc_filter(h);
         if (rc) return rc;
@@ -1539,7 +1728,8 @@ static int compress_now(gcc_forest* h, const char* name = "compress") {
         } else if (!rc) {
             rc = launch_k(h, name, 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)), dim3(kBlock), 0,
                           h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
-                          h->d_giant + (h->giant_slot ^ 1), h->d_bits, clear);
+                          h->d_giant + (h->giant_slot ^ 1), h->d_bits, clear, oth);
+            if (oth_done) *oth_done = oth != nullptr;
         }
         h->giant_slot ^= 1;
         h->has_giant = true;
@@ -1565,7 +1755,7 @@ static int refresh_now(gcc_forest* h) {
     if (!rc)
         rc = launch_k(h, "refresh_bits", 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)),
                       dim3(kBlock), 0, h->d_parent, (u32*)nullptr, h->cap, (const u32*)(h->d_giant + h->giant_slot),
-                      h->d_giant + (h->giant_slot ^ 1), h->d_bits, (u32*)nullptr);
+                      h->d_giant + (h->giant_slot ^ 1), h->d_bits, (u32*)nullptr, (u64*)nullptr);
     if (rc) return rc;
     h->giant_slot ^= 1;
     h->has_giant = true;
@@ -2227,6 +2417,7 @@ int gcc_forest_destroy(gcc_forest* h) {
     }
     if (h->d_scratch) (void)hipFree(h->d_scratch);
     if (h->d_witness) (void)hipFree(h->d_witness);
+    if (h->d_msg_oth) (void)hipFree(h->d_msg_oth);
     if (h->d_bits) (void)hipFree(h->d_bits);
     if (h->d_bloom) (void)hipFree(h->d_bloom);
     if (h->d_giant) (void)hipFree(h->d_giant);
@@ -2325,6 +2516,7 @@ int gcc_forest_reset(gcc_forest* h) {
     h->pending_reset = true;  // materialised lazily (see gcc_forest::pending_reset)
     h->rec_all = false;
     h->host_valid = false;
+    ++h->version;
     h->compressed = true;  // all UNSEEN is canonical
     h->has_giant = false;  // the giant bitmap described the old forest
     h->filter_off = false;
@@ -2366,6 +2558,7 @@ int gcc_forest_union(gcc_forest* h, uint32_t u, uint32_t v) {
     s[2 * h->staged + 1] = v;
     h->staged++;
     h->host_valid = false;
+    ++h->version;
     if (h->staged == gcc_forest::kStageEdges) return submit_slot(h, h->staged);
     return GCC_OK;
 }
@@ -2397,6 +2590,7 @@ int gcc_forest_fold_host(gcc_forest* h, const uint32_t* pairs, uint64_t n_edges)
         }
     }
     h->host_valid = false;
+    ++h->version;
     return flush(h);
 }
 
@@ -2454,6 +2648,7 @@ int gcc_forest_fold_pinned(gcc_forest* h, const uint32_t* pairs, uint64_t n_edge
         HIP_TRY(hipEventRecord(h->pin_folded[s], h->stream));
     }
     h->host_valid = false;
+    ++h->version;
     return GCC_OK;
 }
 
@@ -2483,6 +2678,7 @@ int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, u
                        d_labels, n);
     HIP_TRY(hipGetLastError());
     into->host_valid = false;
+    ++into->version;
     into->compressed = false;
     into->rec_all = false;
     return GCC_OK;
@@ -2549,19 +2745,56 @@ int gcc_forest_encode(gcc_forest* h, void* d_msg, uint64_t cap_others) {
     CHECK_ARG(h && d_msg, "null argument");
     CHECK_ARG((reinterpret_cast<uintptr_t>(d_msg) & 15) == 0, "message buffer must be 16-byte aligned");
     DeviceGuard g(h->device);
-    int rc = compress_async(h);
+    int rc = flush(h);
     if (rc) return rc;
     u32* hdr = reinterpret_cast<u32*>(d_msg);
     u64* bits = reinterpret_cast<u64*>(static_cast<char*>(d_msg) + GCC_MSG_HEADER_BYTES);
-    u32* others = reinterpret_cast<u32*>(bits + ((u64)h->cap + 63) / 64);
-    if (!h->d_witness) HIP_TRY(hipMalloc((void**)&h->d_witness, kMaxPeers * sizeof(u32)));
-    hipLaunchKernelGGL(msg_header_kernel, dim3(1), dim3(kMaxPeers), 0, h->stream, hdr,
-                       h->d_giant ? h->d_giant + h->giant_slot : hdr, h->has_giant ? 1u : 0u, h->cap, h->d_witness);
-    h->witness_armed = true;
     const u64 nw = ((u64)h->cap + 63) / 64;
-    hipLaunchKernelGGL(msg_encode_kernel, dim3((unsigned)((nw + kMsgWordsPerBlock - 1) / kMsgWordsPerBlock)), dim3(kBlock),
-                       0, h->stream, h->d_parent, h->cap, hdr, bits, others, (u64)cap_others);
+    u32* others = reinterpret_cast<u32*>(bits + nw);
+    const u32 nb = (u32)((nw + kMsgWordsPerBlock - 1) / kMsgWordsPerBlock);
+    if (!h->d_witness) HIP_TRY(hipMalloc((void**)&h->d_witness, kMaxPeers * sizeof(u32)));
+    if (!h->d_msg_oth) {  // encode scratch: the others' masks, then per count block its count and list base
+        HIP_TRY(hipMalloc((void**)&h->d_msg_oth, nw * sizeof(u64) + 2 * (size_t)nb * sizeof(u32)));
+    }
+    u32* cnt = reinterpret_cast<u32*>(h->d_msg_oth + nw);
+    u32* base = cnt + nb;
+    // An uncompressed forest is compressed first, by a compress that also writes the others' masks (one pass
+    // over parent[]), so the encode only reads the 8-B masks. Without the giant filter (no masks from the
+    // compress), it is encoded from its parent pointers (read-only finds). Either way the forest's
+    // tracked-component bitmap and root end up exactly what the encode saw, so an absorb right after it can take
+    // "seen" = bitmap | the others' masks without loading parent[].
+    bool masks = false;
+    if (!h->compressed && h->filter_enabled()) {
+        rc = compress_now(h, "compress", h->d_msg_oth, &masks);
+        if (rc) return rc;
+    }
+    const bool find = !h->compressed;
+    const bool track = h->has_giant && h->d_bits && h->d_giant;
+    hipLaunchKernelGGL(msg_header_kernel, dim3(1), dim3(kMaxPeers), 0, h->stream, hdr,
+                       h->d_giant ? h->d_giant + h->giant_slot : hdr, h->has_giant ? 1u : 0u, h->cap, h->d_witness,
+                       (const u32*)h->d_parent, track ? h->d_giant + (h->giant_slot ^ 1) : nullptr);
+    h->witness_armed = true;
+    u64* mine = track ? h->d_bits : nullptr;
+    const u32* gprev = track ? (const u32*)(h->d_giant + h->giant_slot) : nullptr;
+    if (masks && track)
+        hipLaunchKernelGGL(msg_cnt_kernel, dim3(nb), dim3(kBlock), 0, h->stream, (const u64*)h->d_msg_oth,
+                           (const u64*)h->d_bits, bits, nw, cnt);
+    else if (find)
+        hipLaunchKernelGGL(msg_count_kernel<true>, dim3(nb), dim3(kMsgBlock), 0, h->stream, (const u32*)h->d_parent,
+                           h->cap, (const u32*)hdr, gprev, bits, mine, h->d_msg_oth, cnt);
+    else
+        hipLaunchKernelGGL(msg_count_kernel<false>, dim3(nb), dim3(kMsgBlock), 0, h->stream, (const u32*)h->d_parent,
+                           h->cap, (const u32*)hdr, gprev, bits, mine, h->d_msg_oth, cnt);
+    hipLaunchKernelGGL(msg_scan_kernel, dim3(1), dim3(kScanBlock), 0, h->stream, (const u32*)cnt, nb, base, hdr);
+    if (find)
+        hipLaunchKernelGGL(msg_write_kernel<true>, dim3(nb), dim3(kBlock), 0, h->stream, (const u32*)h->d_parent, h->cap,
+                           (const u64*)h->d_msg_oth, (const u32*)base, (const u32*)hdr, gprev, others, (u64)cap_others);
+    else
+        hipLaunchKernelGGL(msg_write_kernel<false>, dim3(nb), dim3(kBlock), 0, h->stream, (const u32*)h->d_parent, h->cap,
+                           (const u64*)h->d_msg_oth, (const u32*)base, (const u32*)hdr, gprev, others, (u64)cap_others);
     HIP_TRY(hipGetLastError());
+    if (track) h->giant_slot ^= 1;  // the header kernel stored the tracked component's current root there
+    h->enc_version = h->version;
     return GCC_OK;
 }
 
@@ -2592,7 +2825,8 @@ int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_by
     if (tracked)
         hipLaunchKernelGGL(msg_absorb_bits_kernel, dim3(grid_for(nw * 64, kMaxGrid)), dim3(kBlock), 0, h->stream,
                            h->d_parent, msgs, (u64)stride_bytes, count, skip, h->cap, mine,
-                           (const u32*)(h->d_giant + h->giant_slot), (const u32*)h->d_witness);
+                           (const u32*)(h->d_giant + h->giant_slot), (const u32*)h->d_witness,
+                           h->enc_version == h->version ? (const u64*)h->d_msg_oth : nullptr);
     hipLaunchKernelGGL(msg_absorb_kernel, dim3(grid_for(work, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent, msgs,
                        (u64)stride_bytes, count, skip, (u64)cap_others, h->cap, tracked,
                        tracked ? (const u32*)h->d_witness : nullptr);

@@ -38,6 +38,16 @@ def main():
                 per.append((time.perf_counter() - t0) * 1e3)
             fold_ms.append(max(per))
             torch.cuda.synchronize()
+            if rep == 0:  # the compact message each rank would send: header + giant bitmap + (v, label) of the others
+                import numpy as np
+                msg = []
+                for ds in forests:
+                    lab = ds.labels()
+                    seen = lab[lab != 0xFFFFFFFF]
+                    giant = int(np.bincount(seen).max()) if seen.size else 0
+                    msg.append(16 + V // 8 + 8 * (seen.size - giant))
+                print(f"P={P}: message bytes per rank max {max(msg)} (bitmap {V // 8}, list {max(msg) - 16 - V // 8})",
+                      flush=True)
             t0 = time.perf_counter()
             group_merge(forests)
             for ds in forests:
