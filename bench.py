@@ -176,7 +176,9 @@ def kernel_stats(log, V, inst_steps):
                  "seed_filter": "slice_filter_kernel<false>", "slice_hook": "slice_hook_kernel<true>",
                  "seed_hook": "slice_hook_kernel<false>", "bucket_hook": "bucket_hook_kernel",
                  "bucket_slow": "bucket_slow_kernel", "bucket_rest": "bucket_rest_kernel",
-                 "bucket_layout": "bucket_layout_kernel", "bucket_hub": "bucket_hub_kernel", "bucket_init": "bucket_init_kernel", "overflow": "fold_filtered_kernel"}
+                 "bucket_layout": "bucket_layout_kernel", "bucket_hub": "bucket_hub_kernel", "bucket_init": "bucket_init_kernel", "overflow": "fold_filtered_kernel",
+                 "slice_filter2": "slice_filter_kernel<true,true>", "slice_hook2": "slice_hook_kernel<true> (level 2)",
+                 "bucket_hook2": "bucket_hook_kernel (level 2)"}
     phases, kernels, spans = {}, {}, []
     for name, ms, n in log:
         if name in ("begin", "slow_edges"):

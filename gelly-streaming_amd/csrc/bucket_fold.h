@@ -49,8 +49,16 @@ struct Meta {
     u32 ovf_cur;                 // overflow list cursor (may pass its capacity: then `spill`)
     u32 spill;                   // 1: some edge fit neither its bucket nor the overflow list
     u32 gmin;                    // min C (seeding)
-    u32 pad;
+    u32 nseg;                    // FINAL P2: slow-list segments recorded (SlowSeg table)
     u32 slow_cnt[kMaxP2Blocks];  // FINAL P2: slow edges (source not in C) each block listed in its own region
+};
+
+// A run of one P2 block's slow list whose edges share a source slice (one P2 item's slow edges): the second
+// filter level (slice_filter_kernel<true, true>) takes these runs as its items. off is even (runs padded to pairs).
+struct SlowSeg {
+    u64 off;  // first entry, in the whole slow array
+    u32 sl;   // source slice
+    u32 len;  // entries (a ~0 tail entry pads an odd run)
 };
 
 __device__ __forceinline__ u32 lds_bit(const u32* s, u32 x) { return (s[x >> 5] >> (x & 31)) & 1u; }
@@ -180,6 +188,7 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     block_prefix(m->bk_cap, m->bk_base, ns, s_scan);
     block_prefix(m->vl_cap, m->vl_base, ns, s_scan);
     if (threadIdx.x < 16) m->work[threadIdx.x] = 0;
+    if (threadIdx.x == 0) m->nseg = 0;
     if (threadIdx.x == 0) {
         m->ovf_cur = 0;
         m->spill = 0;
@@ -361,13 +370,18 @@ __device__ __forceinline__ void hook_g(u32* parent, u32 g, u32 v) {
 // capacity came from a sample): FINAL hooks v under g right here, SEED drops it (seeding is only a heuristic).
 // Rounds of kP2Round edges, the next round's loads in flight; counters double-buffered (3 barriers per round).
 // LDS: slice (64 KiB) + v tile (kP2Round u32) + counters + layout + rings (FINAL).
-template <bool FINAL>
+// SEG (second level, FINAL only): the items are the slow-list runs the FINAL pass recorded (`segs`, m->nseg of
+// them; `bk` = the slow array), C is then C | N, and its own slow edges go to `slow` (the bucket storage, free
+// by then). FINAL without SEG records those runs into `segs` (one per item with slow edges; null: none).
+template <bool FINAL, bool SEG = false>
 __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict__ parent, const u64* __restrict__ bk,
                                                                 const u32* __restrict__ bits, u32 nwords32, u32 ns,
                                                                 Meta* __restrict__ m, u32* __restrict__ vl, u32 cps,
                                                                 u32 frac, u32 work_slot, u32 drain_at,
                                                                 const u32* __restrict__ giant, u64* __restrict__ slow,
-                                                                u32 slow_cap, u32 cap, u32* __restrict__ err) {
+                                                                u32 slow_cap, u32 cap, u32* __restrict__ err,
+                                                                SlowSeg* __restrict__ segs) {
+    static_assert(FINAL || !SEG, "the second level is a FINAL pass");
     trace_start(FINAL ? kTrBkP2 : kTrBkP2Seed);
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     u32* s_bits = s_dyn;                                   // kSliceWords
@@ -397,25 +411,57 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         runs.cpos[s] = runs.cend[s] = 0;
     }
     if (threadIdx.x == 0) s_slow = 0;
-    const u32 n_items = ns * cps;
+    const u32 n_items = SEG ? m->nseg : ns * cps;
+    // thread 0: the open slow-list run of the current item (FINAL, recording)
+    u32 seg_sl = 0xFFFFFFFFu, seg_start = 0;
+    auto close_seg = [&]() {  // thread 0, after a barrier (every wave's slow stores of the item are done)
+        if (!FINAL || SEG || !segs || seg_sl == 0xFFFFFFFFu) return;
+        u32 end = s_slow;
+        if (end & 1u) {  // pad to a pair: the next run starts 16-B aligned
+            if (end < slow_cap) my_slow[end] = ~0ull;
+            s_slow = ++end;
+        }
+        end = end < slow_cap ? end : slow_cap;
+        if (end > seg_start) {
+            const u32 k = atomicAdd(&m->nseg, 1u);
+            segs[k] = SlowSeg{(u64)blockIdx.x * slow_cap + seg_start, seg_sl, end - seg_start};
+        }
+        seg_sl = 0xFFFFFFFFu;
+    };
     while (true) {
         __syncthreads();
-        if (threadIdx.x == 0) s_item = atomicAdd(&m->work[work_slot], 1u);
+        if (threadIdx.x == 0) {
+            close_seg();
+            seg_start = s_slow;  // stable here: the item's waves add to s_slow only after the next barrier
+            s_item = atomicAdd(&m->work[work_slot], 1u);
+        }
         __syncthreads();
         const u32 item = s_item;
         if (item >= n_items) break;
-        const u32 sl = item / cps;
-        u64 len = m->bk_cur[sl] < m->bk_cap[sl] ? m->bk_cur[sl] : m->bk_cap[sl];
-        if (!FINAL) len = len * frac >> 16;
-        u64 lo, hi;
-        item_range(len, item % cps, cps, lo, hi);
+        u32 sl;
+        u64 len, lo, hi;
+        const u64* src = bk;
+        if constexpr (SEG) {
+            const SlowSeg sg = segs[item];
+            sl = sg.sl;
+            src = bk + sg.off;
+            lo = 0;
+            hi = len = sg.len;
+        } else {
+            sl = item / cps;
+            len = m->bk_cur[sl] < m->bk_cap[sl] ? m->bk_cur[sl] : m->bk_cap[sl];
+            if (!FINAL) len = len * frac >> 16;
+            item_range(len, item % cps, cps, lo, hi);
+            src = bk + m->bk_base[sl];
+        }
         if (lo >= hi) continue;
+        if (threadIdx.x == 0) seg_sl = sl;
         if (sl != cur_slice) {
             load_slice<kP2Block>(s_bits, bits, sl, nwords32);
             cur_slice = sl;
             __syncthreads();
         }
-        const u4* eb = reinterpret_cast<const u4*>(bk + m->bk_base[sl]);  // 16-B aligned (16-edge capacities)
+        const u4* eb = reinterpret_cast<const u4*>(src);  // 16-B aligned (16-edge capacities; runs padded to pairs)
         const u32 sbase = sl << kSliceBits;
         // pairs [lo / 2, ceil(hi / 2)); edges outside [lo, hi) are masked (a part may start or end mid-pair)
         const u64 plo = lo / 2;
@@ -663,6 +709,7 @@ __global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ p
     const u64* list = slow + (u64)r * slow_cap;
     for (u32 k = part * kBlock + threadIdx.x; k < cnt; k += kSlowSplit * kBlock) {
         const u64 e = list[k];
+        if (e == ~0ull) continue;  // a run's pad entry (slice_filter_kernel's close_seg)
         const u32 a = (u32)e, b = (u32)(e >> 32);
         if (a >= cap || b >= cap) {
             flag_err(err, kErrSlow);

@@ -1471,6 +1471,7 @@ struct FoldTune {
     int bucket_levels = 3;
     double bucket_sample = 0.15;  // profiles/r2_sweep_c4_p1.log: 0.25 -> 0.15 = 12.74 -> 12.22 ms on C4
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
+    int bucket_slow2 = 1;        // second filter level over the slow edges with C | N (C4's 1/8 share: 19 % slow edges)
     int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
@@ -1551,6 +1552,8 @@ struct gcc_forest {
     u64* d_slow = nullptr;  // FINAL P2's slow edges, one region per block
     u64 slow_cap_total = 0;
     u32* d_nbits = nullptr;  // N: ids reached from C by the FINAL pass (kept all-zero between batches)
+    bk::SlowSeg* d_seg = nullptr;  // FINAL P2's slow-list runs (the second filter level's items)
+    u64 seg_cap = 0;
 
     // lazy host view of the labels (getMatches()/find() consumers)
     std::vector<u32> host_labels;
@@ -1962,7 +1965,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if ((rc = grow(h->d_vl, h->vl_cap, bk::storage_edges(n, ns, p2_blocks), h->stream))) return rc;
     // room for half the batch in the slow lists (C4: 3.9 % slow; C4's 1/8 share: more than the 12.5 % an n/8
     // capacity held, and the rest took P2's inline ring unions: 1.03 ms instead of ~0.5)
-    const u32 slow_cap = (u32)std::min<u64>(0x7FFFFFFFull, std::max<u64>(4096, n / p2_blocks / 2));
+    const u32 slow_cap = (u32)std::min<u64>(0x7FFFFFFEull, std::max<u64>(4096, n / p2_blocks / 2)) & ~1u;  // even: runs pair-aligned
     if ((rc = grow(h->d_slow, h->slow_cap_total, (u64)p2_blocks * slow_cap, h->stream))) return rc;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
     u32* bits = reinterpret_cast<u32*>(h->d_bits);
@@ -1977,6 +1980,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u32 cps = std::max<u32>(1, (items + ns - 1) / ns);
     // A block loads a part's 64 KiB bitmap slice into LDS per item: a pass over few edges (the seeding levels of a
     // small batch) takes fewer, longer parts, about 64K edges per part at least
+    const bool slow2 = t.bucket_slow2 != 0;
+    if (slow2 && (rc = grow(h->d_seg, h->seg_cap, (u64)ns * cps + 64, h->stream))) return rc;
     const u32 cps_seed = (u32)std::max<u64>(1, std::min<u64>(cps, (u64)((double)n * t.bucket_sample) / ((u64)ns << 16)));
     const size_t f_lds = slice_filter_lds(), h_lds = bk::kSliceWords * sizeof(u32);
     const size_t vl_cur_off = offsetof(bk::Meta, vl_cur);
@@ -2001,7 +2006,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
         rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
                       f_lds, h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps_seed, frac,
-                      slot++, h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err);
+                      slot++, h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err,
+                      (bk::SlowSeg*)nullptr);
         if (!rc)
             rc = launch_k(h, "seed_hook", 0, bk::slice_hook_kernel<false>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
                           bits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps_seed, slot++, h->cap, h->d_err);
@@ -2014,16 +2020,37 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
     rc = launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true>, dim3(p2_blocks), dim3(bk::kP2Block), f_lds,
                   h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps, 65536u, slot++,
-                  h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err);
+                  h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr);
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
                       h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
     if (!rc)
         rc = launch_k(h, "bucket_hook", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
                       h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
+    // Second level over the slow edges, now against C | N: a slow edge whose source joined N is a hook of its
+    // target (its v-list again), only the rest stays slow. Its input is FINAL P2's slow runs (one source slice
+    // each); its slow edges go to the bucket storage, which P2 has consumed.
+    const u64* slow_list = h->d_slow;
+    u32 slow_list_cap = slow_cap;
+    if (slow2 && !rc) {
+        const u32 slow_cap2 = (u32)std::min<u64>(0x7FFFFFFEull, h->bk_cap_edges / p2_blocks) & ~1u;
+        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
+        rc = launch_k(h, "slice_filter2", 0, bk::slice_filter_kernel<true, true>, dim3(p2_blocks), dim3(bk::kP2Block),
+                      f_lds, h->d_parent, (const u64*)h->d_slow, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, 1u,
+                      65536u, slot++, h->tune.drain_at, (const u32*)giant, h->d_bk, slow_cap2, h->cap, h->d_err, h->d_seg);
+        if (!rc)
+            rc = launch_k(h, "slice_hook2", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
+                          h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
+        if (!rc)
+            rc = launch_k(h, "bucket_hook2", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
+                          h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
+        slow_list = h->d_bk;
+        slow_list_cap = slow_cap2;
+    }
     if (!rc)
-        rc = launch_k(h, "bucket_slow", 0, bk::bucket_slow_kernel, dim3(p2_blocks * bk::kSlowSplit), dim3(kBlock), 0, h->d_parent, (const u64*)h->d_slow, slow_cap, (const bk::Meta*)h->d_meta, p2_blocks,
-                      (const u32*)bits, (const u32*)giant, h->cap, h->d_err);
+        rc = launch_k(h, "bucket_slow", 0, bk::bucket_slow_kernel, dim3(p2_blocks * bk::kSlowSplit), dim3(kBlock), 0,
+                      h->d_parent, slow_list, slow_list_cap, (const bk::Meta*)h->d_meta, p2_blocks, (const u32*)bits,
+                      (const u32*)giant, h->cap, h->d_err);
     if (!rc)
         rc = launch_k(h, "bucket_rest", 0, bk::bucket_rest_kernel, dim3(grid_for(n / 64 + 1, kMaxGrid)), dim3(kBlock), 0,
                       h->d_parent, (const u64*)h->d_ovf, ovf_cap, (const bk::Meta*)h->d_meta, (const u32*)bits, edges, n,
@@ -2326,6 +2353,7 @@ static int set_lds_attrs_impl() {
         {(const void*)seed_bfs_kernel<true, kFilterBlockLds, false, true>, bitmap},
         {(const void*)bk::slice_filter_kernel<false>, (int)slice_filter_lds()},
         {(const void*)bk::slice_filter_kernel<true>, (int)slice_filter_lds()},
+        {(const void*)bk::slice_filter_kernel<true, true>, (int)slice_filter_lds()},
         {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kSliceWords * sizeof(u32))},
         {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kSliceWords * sizeof(u32))},
         {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
@@ -2417,6 +2445,7 @@ int gcc_forest_destroy(gcc_forest* h) {
     }
     if (h->d_scratch) (void)hipFree(h->d_scratch);
     if (h->d_witness) (void)hipFree(h->d_witness);
+    if (h->d_seg) (void)hipFree(h->d_seg);
     if (h->d_msg_oth) (void)hipFree(h->d_msg_oth);
     if (h->d_bits) (void)hipFree(h->d_bits);
     if (h->d_bloom) (void)hipFree(h->d_bloom);
@@ -3063,6 +3092,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "inc_div") t.inc_div = std::max<u64>(1, (u64)value);
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = (int)value == 1 ? 1 : 0;
+    else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
     else if (k == "bucket") t.bucket = value != 0;
     else if (k == "bucket_min_batch") t.bucket_min_batch = (u64)value;
     else if (k == "bucket_min_ids") t.bucket_min_ids = (u64)value;
