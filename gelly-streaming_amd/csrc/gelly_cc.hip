@@ -544,7 +544,8 @@ static inline unsigned chunk_grid(u64 n, int per_wave, int block, unsigned max_b
 __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__ parent, u32* __restrict__ labels, u32 n,
                                                                const u32* __restrict__ giant_prev,
                                                                u32* __restrict__ giant_next, u64* __restrict__ bits,
-                                                               u32* __restrict__ bloom_clear, u64* __restrict__ oth) {
+                                                               u32* __restrict__ bloom_clear, u64* __restrict__ oth,
+                                                               const u64* __restrict__ newbits) {
     trace_start(kTrCompressBits);
     __shared__ u32 s_g, s_g0;
     NoCount c;
@@ -593,6 +594,14 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
             lab[1] = (p.y >= v0 + 1 || p.y == g) ? p.y : (p.y == g0 ? g : UF::find_from(parent, v0 + 1, p.y, c));
             lab[2] = (p.z >= v0 + 2 || p.z == g) ? p.z : (p.z == g0 ? g : UF::find_from(parent, v0 + 2, p.z, c));
             lab[3] = (p.w >= v0 + 3 || p.w == g) ? p.w : (p.w == g0 ? g : UF::find_from(parent, v0 + 3, p.w, c));
+            if (newbits) {  // an absorb's deferred new ids (msg_absorb_bits_kernel): still UNSEEN, in g's component
+                const u32 nb = (u32)(newbits[v0 >> 6] >> (v0 & 63)) & 15u;
+                if (nb) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (((nb >> k) & 1u) && lab[k] == UNSEEN) lab[k] = g;
+                }
+            }
             if (labels) {
                 const u32x4 o = {lab[0], lab[1], lab[2], lab[3]};
                 *reinterpret_cast<u32x4*>(labels + v0) = o;
@@ -607,6 +616,7 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
         for (u32 k = 0; k < 4; ++k)
             if (v0 + k < n) {
                 lab[k] = gcc::compress_label(parent, (u32)(v0 + k));
+                if (newbits && lab[k] == UNSEEN && ((newbits[(v0 + k) >> 6] >> ((v0 + k) & 63)) & 1ull)) lab[k] = g;
                 if (labels) labels[v0 + k] = lab[k];
             }
         if (bits) chunk_bits(bits, nwords, nfull, lane, g, lab);
@@ -1258,7 +1268,8 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict
                                                                  const u64* __restrict__ mine,
                                                                  const u32* __restrict__ tracked,
                                                                  const u32* __restrict__ witness,
-                                                                 const u64* __restrict__ seen_oth) {
+                                                                 const u64* __restrict__ seen_oth,
+                                                                 u64* __restrict__ newbits) {
     __shared__ u32 s_g[kMaxPeers];
     __shared__ u32 s_w[kMaxPeers];
     msg_peers(msgs, stride, count, skip, n, true, witness, s_g, s_w);
@@ -1280,6 +1291,28 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict
                     m |= reinterpret_cast<const u64*>(msgs + p * stride + GCC_MSG_HEADER_BYTES)[w];
             if (m) m &= ~mine[w];
             if (m && seen_oth) so = seen_oth[w];
+        }
+        if (newbits) {  // deferred: the new ids above R only go into newbits, the compress right after labels them
+            u64 nb = 0, seen_todo = 0;
+            if (w < nw) {
+                const u64 above = (R >= w * 64 + 63) ? 0ull
+                                : (R < w * 64 ? ~0ull : (~0ull << (R - w * 64)) << 1);  // ids > R of this word
+                nb = m & ~so & above;
+                seen_todo = m & ~nb;  // seen outside T (or a new id below R): the union
+                newbits[w] = nb;      // overwrites this word's mask (read above, same lane)
+            }
+            unsigned long long sw = __ballot(seen_todo != 0);
+            while (sw) {
+                const int j = __builtin_ctzll(sw);
+                sw &= sw - 1;
+                const u64 t = __shfl(seen_todo, j, 64);
+                const u32 v = (u32)((w0 + (u64)j) * 64 + lane);
+                if ((t >> lane) & 1ull) {
+                    NoCount c;
+                    UF::unite(parent, v, R, c);
+                }
+            }
+            continue;
         }
         unsigned long long todo_words = __ballot(m != 0);
         if (seen_oth) {  // the encode's masks say which ids outside T are seen: the others are new, no load needed
@@ -1328,7 +1361,9 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict
 // (each id against its own root g_p) and every peer's (v, label) list.
 __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ parent, const char* __restrict__ msgs,
                                                             u64 stride, u32 count, u32 skip, u64 cap, u32 n,
-                                                            bool tracked, const u32* __restrict__ witness) {
+                                                            bool tracked, const u32* __restrict__ witness,
+                                                            const u64* __restrict__ newbits,
+                                                            const u32* __restrict__ tracked_root) {
     __shared__ u32 s_g[kMaxPeers];
     __shared__ u32 s_w[kMaxPeers];
     msg_peers(msgs, stride, count, skip, n, tracked, witness, s_g, s_w);
@@ -1347,12 +1382,18 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
                 lone = reinterpret_cast<const u64*>(msgs + lane * stride + GCC_MSG_HEADER_BYTES)[w];
             const u64 v = w * 64 + lane;
             unsigned long long lb = __ballot(lone != 0);
+            bool in_lone = false;
             while (lb) {
                 const u32 p = (u32)__builtin_ctzll(lb);
                 lb &= lb - 1;
                 const u64 mp = __shfl(lone, (int)p, 64);
-                if (((mp >> lane) & 1ull) && (u32)v != s_g[p]) UF::unite(parent, (u32)v, s_g[p], c);
+                if ((mp >> lane) & 1ull) {
+                    in_lone = true;
+                    if ((u32)v != s_g[p]) UF::unite(parent, (u32)v, s_g[p], c);
+                }
             }
+            // a deferred new id (absorb_bits' newbits) in a lone giant: that union made it seen, so it joins R here
+            if (in_lone && newbits && v < n && ((newbits[w] >> lane) & 1ull)) UF::unite(parent, (u32)v, *tracked_root, c);
         }
     }
     // the lists as one flat index over (peer, entry): one header load per entry, every union in flight at once
@@ -1365,7 +1406,13 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
         if (hdr[2] != n || k >= min((u64)hdr[1], cap)) continue;
         const u32* others = reinterpret_cast<const u32*>(msgs + p * stride + GCC_MSG_HEADER_BYTES + nw * sizeof(u64));
         const u32 v = others[2 * k], l = others[2 * k + 1];
-        if (v < n && l < n) UF::unite(parent, v, l, c);
+        if (v < n && l < n) {
+            UF::unite(parent, v, l, c);
+            // a deferred new id (absorb_bits' newbits) is in R's component too: this union made it seen, so the
+            // compress would no longer label it through newbits
+            if (newbits && (((newbits[v >> 6] >> (v & 63)) | (newbits[l >> 6] >> (l & 63))) & 1ull))
+                UF::unite(parent, v, *tracked_root, c);
+        }
     }
 }
 
@@ -1697,14 +1744,17 @@ static bool inc_forest(const gcc_forest* h) {
 // Incremental (compress_inc_kernel) when every mutation since the last compress was recorded.
 // oth (the merge encode): a full compress also writes the others mask of every 64-id word (chunk_oth); returns
 // whether it did (only the full compress of a filtered forest can).
-static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth = nullptr, bool* oth_done = nullptr) {
+// newbits (gcc_forest_absorb_many): ids still UNSEEN that belong to the tracked component (a full compress of a
+// filtered forest; the caller checks).
+static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth = nullptr, bool* oth_done = nullptr,
+                        const u64* newbits = nullptr) {
     int rc = GCC_OK;
     bool inplace = false;  // the compress rewrote d_parent itself (no swap)
-    const bool inc_here = inc_forest(h) && !oth;  // the encode wants the masks: a full compress
+    const bool inc_here = inc_forest(h) && !oth && !newbits;  // masks in or out: a full compress
     if (!h->filter_enabled()) {
         rc = launch_k(h, name, 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)), dim3(kBlock), 0,
                       h->d_parent, h->d_spare, h->cap, (const u32*)nullptr, (u32*)nullptr, (u64*)nullptr, (u32*)nullptr,
-                      (u64*)nullptr);
+                      (u64*)nullptr, (const u64*)nullptr);
     } else {
         rc = alloc_filter(h);
         if (rc) return rc;
@@ -1731,7 +1781,7 @@ static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth =
         } else if (!rc) {
             rc = launch_k(h, name, 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)), dim3(kBlock), 0,
                           h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
-                          h->d_giant + (h->giant_slot ^ 1), h->d_bits, clear, oth);
+                          h->d_giant + (h->giant_slot ^ 1), h->d_bits, clear, oth, newbits);
             if (oth_done) *oth_done = oth != nullptr;
         }
         h->giant_slot ^= 1;
@@ -1758,7 +1808,7 @@ static int refresh_now(gcc_forest* h) {
     if (!rc)
         rc = launch_k(h, "refresh_bits", 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)),
                       dim3(kBlock), 0, h->d_parent, (u32*)nullptr, h->cap, (const u32*)(h->d_giant + h->giant_slot),
-                      h->d_giant + (h->giant_slot ^ 1), h->d_bits, (u32*)nullptr, (u64*)nullptr);
+                      h->d_giant + (h->giant_slot ^ 1), h->d_bits, (u32*)nullptr, (u64*)nullptr, (const u64*)nullptr);
     if (rc) return rc;
     h->giant_slot ^= 1;
     h->has_giant = true;
@@ -2851,16 +2901,23 @@ int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_by
     // one list entry per lane; with no tracked component every giant goes id by id too (one word per wave)
     const u64 lists = std::max<u64>((u64)count * cap_others, 1);
     const u64 work = tracked ? std::max<u64>(lists, 64 * kBlock) : std::max<u64>(nw * 64, lists);
+    // With the encode's masks (this forest's seen ids outside T), the new ids above R are not stored one by one:
+    // they go into `newbits` (the masks' words, overwritten) and the compress that follows right here labels them
+    // with R's root as it writes every label anyway (one pass over parent[] less). Until that compress the forest
+    // is not a valid forest: it runs before this call returns.
+    const bool masks = tracked && h->d_msg_oth && h->enc_version == h->version;
+    u64* newbits = (masks && h->filter_enabled()) ? h->d_msg_oth : nullptr;
+    const u32* troot = tracked ? (const u32*)(h->d_giant + h->giant_slot) : nullptr;
     if (tracked)
         hipLaunchKernelGGL(msg_absorb_bits_kernel, dim3(grid_for(nw * 64, kMaxGrid)), dim3(kBlock), 0, h->stream,
-                           h->d_parent, msgs, (u64)stride_bytes, count, skip, h->cap, mine,
-                           (const u32*)(h->d_giant + h->giant_slot), (const u32*)h->d_witness,
-                           h->enc_version == h->version ? (const u64*)h->d_msg_oth : nullptr);
+                           h->d_parent, msgs, (u64)stride_bytes, count, skip, h->cap, mine, troot,
+                           (const u32*)h->d_witness, masks ? (const u64*)h->d_msg_oth : nullptr, newbits);
     hipLaunchKernelGGL(msg_absorb_kernel, dim3(grid_for(work, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent, msgs,
                        (u64)stride_bytes, count, skip, (u64)cap_others, h->cap, tracked,
-                       tracked ? (const u32*)h->d_witness : nullptr);
+                       tracked ? (const u32*)h->d_witness : nullptr, (const u64*)newbits, troot);
     HIP_TRY(hipGetLastError());
     mark_mutated(h);
+    if (newbits) return compress_now(h, "compress", nullptr, nullptr, newbits);
     return GCC_OK;
 }
 
