@@ -83,7 +83,7 @@ def test_forest_group_ranks_share_one_gpu(mode, world):
 
 
 # ---- the group merge behind the C ABI (csrc/gelly_group.cpp) ----
-def _windows_vs_oracle(cfg, starts, P, merge):
+def _windows_vs_oracle(cfg, starts, P, merge, knobs=None):
     import oracle as orc
     import torch
     from gelly_stream import DisjointSet
@@ -95,6 +95,9 @@ def _windows_vs_oracle(cfg, starts, P, merge):
     G.generate_device(cfg, 0, E, d.data_ptr(), 0)
     torch.cuda.synchronize()
     forests = [DisjointSet(V) for _ in range(P)]
+    for ds in forests:
+        if knobs:
+            ds.tune(**knobs)
     for w in range(len(starts) - 1):
         b, e = int(starts[w]), int(starts[w + 1])
         for r, ds in enumerate(forests):  # rank r folds its contiguous 1/P of the window (bench.py's partitioning)
@@ -118,6 +121,17 @@ def test_c_abi_group_merge_one_device(P):
     cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=17, n_edges=1 << 20, seed=0x6770)
     starts = np.asarray([0, 1000, 1 << 17, 1 << 19, 1 << 20], dtype=np.uint64)
     _windows_vs_oracle(cfg, starts, P, group_merge)
+
+
+def test_c_abi_group_merge_unfiltered_forests():
+    """Forests without the giant filter are encoded straight from their parent pointers (msg_count_kernel<true>:
+    read-only finds, no compress first) and absorb without deferred ids."""
+    from gelly_stream import generators as G
+    from gelly_stream.distributed import group_merge
+
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=17, n_edges=1 << 19, seed=0x6771)
+    starts = np.asarray([0, 1000, 1 << 17, 1 << 19], dtype=np.uint64)
+    _windows_vs_oracle(cfg, starts, 3, group_merge, knobs={"filter": 0})
 
 
 def test_c_abi_group_merge_retry_and_label_fallback():
@@ -176,3 +190,42 @@ def test_c_abi_group_merge_two_devices():
         x.close()
     for x in comms:
         x.close()
+
+
+def test_group_merge_deferred_new_ids():
+    """The absorb defers the new ids of overlapping peer giants to its compress (gcc_forest_absorb_many). Ids that
+    another peer's LONE giant or a peer's (v, label) list also touches become seen before that compress and must
+    still join the tracked component. Four hand-made forests over 2^17 ids (giant filter on), every forest against
+    the oracle's partition of all edges: A's giant [1000, 60000); B's [50000, 110000) overlaps it; C's
+    [110000, 131000) + 70000 does not overlap A but holds one of B's ids; D's giant [200, 900) is lone everywhere and
+    its small components {65000, 130500} and {100, 64000} pair ids of B's and C's giants with new ones."""
+    import oracle as orc
+    from gelly_stream import DisjointSet
+    from gelly_stream.distributed import group_merge
+
+    V = 1 << 17
+
+    def path(ids):
+        ids = np.asarray(ids, dtype=np.uint32)
+        return np.stack([ids[:-1], ids[1:]], axis=1)
+
+    parts = [
+        path(np.arange(1000, 60000)),
+        path(np.arange(50000, 110000)),
+        np.concatenate([path(np.arange(110000, 131000)), np.asarray([[110000, 70000]], dtype=np.uint32)]),
+        np.concatenate([path(np.arange(200, 900)), np.asarray([[65000, 130500], [100, 64000]], dtype=np.uint32)]),
+    ]
+    allp = np.ascontiguousarray(np.concatenate(parts))
+    want = orc.cc_stream(allp, [0, len(allp)], V, partitions=1, want_labels=True)["labels"][0]
+    forests = [DisjointSet(V) for _ in parts]
+    try:
+        for ds, p in zip(forests, parts):
+            ds.fold(np.ascontiguousarray(p))
+            ds.compress()  # elects and tracks each forest's giant
+        group_merge(forests)
+        for r, ds in enumerate(forests):
+            got = ds.labels()
+            assert np.array_equal(got, want), (r, int(np.flatnonzero(got != want)[0]))
+    finally:
+        for ds in forests:
+            ds.close()
