@@ -229,13 +229,18 @@ __device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u
 // order and writes every run out contiguously (runs of ~kP1Tile / ns edges). The next tile's loads are in flight
 // meanwhile. Bad ids: skipped + *err. The odd last edge of an odd-length batch and every edge past its bucket's
 // capacity go to the overflow list.
+// P1's dynamic LDS: the tile in bucket order, every bucket's run padded to an even length — up to one slot per
+// slice beyond the tile. (Round 2 first sized it to the tile alone: a full tile's last padded slots fell past the
+// allocation and relied on the LDS allocation's rounding slack; a 1024 x 8 geometry with less slack lost edges.)
+constexpr size_t p1_lds(int block, int per) { return ((size_t)block * per + kMaxSlicesLds) * sizeof(u64); }
+
 template <int P1B, int P1P>
 __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                           Meta* __restrict__ m, u64* __restrict__ bk,
                                                           u64* __restrict__ ovf, u32 ovf_cap, u32* __restrict__ err) {
     trace_start(kTrBkP1);
-    // the tile in bucket order: dynamic LDS (P1B * P1P u64, 64 / 128 KiB), set up like every kernel's LDS beyond
-    // 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-slice state below is static
+    // the tile in bucket order: dynamic LDS (p1_lds: P1B * P1P + kMaxSlicesLds u64, 66 / 130 KiB), set up like every
+    // kernel's LDS beyond 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-slice state below is static
     extern __shared__ __attribute__((aligned(16))) u64 s_srt[];
     __shared__ u32 s_cnt[kMaxSlicesLds], s_pc[kMaxSlicesLds], s_start[kMaxSlicesLds], s_cap[kMaxSlicesLds];
     __shared__ u32 s_cpos[kMaxSlicesLds], s_cend[kMaxSlicesLds], s_p1[kMaxSlicesLds], s_l1[kMaxSlicesLds],

@@ -2040,9 +2040,9 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                   p1_blocks, p2_blocks);
     if (!rc)
         rc = t.bucket_p1 == 1
-                 ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16>, dim3(h->n_cu), dim3(1024), 1024 * 16 * sizeof(u64),
+                 ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16>, dim3(h->n_cu), dim3(1024), bk::p1_lds(1024, 16),
                             edges, n, ns, h->cap, h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err)
-                 : launch_k(h, "bucket", n, bk::bucket_kernel<512, 16>, dim3(p1_blocks), dim3(512), 512 * 16 * sizeof(u64),
+                 : launch_k(h, "bucket", n, bk::bucket_kernel<512, 16>, dim3(p1_blocks), dim3(512), bk::p1_lds(512, 16),
                             edges, n, ns, h->cap, h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err);
     if (rc) return rc;
     // seeding: C := {hub}, then levels over the sample
@@ -2407,8 +2407,8 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kSliceWords * sizeof(u32))},
         {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kSliceWords * sizeof(u32))},
         {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
-        {(const void*)bk::bucket_kernel<512, 16>, (int)(512 * 16 * sizeof(u64))},
-        {(const void*)bk::bucket_kernel<1024, 16>, (int)(1024 * 16 * sizeof(u64))},
+        {(const void*)bk::bucket_kernel<512, 16>, (int)bk::p1_lds(512, 16)},
+        {(const void*)bk::bucket_kernel<1024, 16>, (int)bk::p1_lds(1024, 16)},
     };
     for (const auto& t : tab) HIP_TRY(hipFuncSetAttribute(t.f, hipFuncAttributeMaxDynamicSharedMemorySize, t.bytes));
     return set_trace_slot();
