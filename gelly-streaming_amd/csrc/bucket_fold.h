@@ -375,6 +375,7 @@ __device__ __forceinline__ void hook_g(u32* parent, u32 g, u32 v) {
 // capacity came from a sample): FINAL hooks v under g right here, SEED drops it (seeding is only a heuristic).
 // Rounds of kP2Round edges, the next round's loads in flight; counters double-buffered (3 barriers per round).
 // LDS: slice (64 KiB) + v tile (kP2Round u32) + counters + layout + rings (FINAL).
+// hub_only (SEED): the first level, C = {h} (m->gmin): only the items of h's slice are streamed.
 // SEG (second level, FINAL only): the items are the slow-list runs the FINAL pass recorded (`segs`, m->nseg of
 // them; `bk` = the slow array), C is then C | N, and its own slow edges go to `slow` (the bucket storage, free
 // by then). FINAL without SEG records those runs into `segs` (one per item with slow edges; null: none).
@@ -382,7 +383,7 @@ template <bool FINAL, bool SEG = false>
 __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict__ parent, const u64* __restrict__ bk,
                                                                 const u32* __restrict__ bits, u32 nwords32, u32 ns,
                                                                 Meta* __restrict__ m, u32* __restrict__ vl, u32 cps,
-                                                                u32 frac, u32 work_slot, u32 drain_at,
+                                                                u32 frac, u32 work_slot, u32 drain_at, u32 hub_only,
                                                                 const u32* __restrict__ giant, u64* __restrict__ slow,
                                                                 u32 slow_cap, u32 cap, u32* __restrict__ err,
                                                                 SlowSeg* __restrict__ segs) {
@@ -416,7 +417,10 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         runs.cpos[s] = runs.cend[s] = 0;
     }
     if (threadIdx.x == 0) s_slow = 0;
-    const u32 n_items = SEG ? m->nseg : ns * cps;
+    // the first seeding level (hub_only): C = {h}, so only h's slice has sources in C: its sample alone, in cps
+    // parts (the other 127 of C4's 128 sample buckets would be streamed for nothing)
+    const u32 hub_sl = (!FINAL && hub_only) ? (m->gmin >> kSliceBits) : 0u;
+    const u32 n_items = SEG ? m->nseg : ((!FINAL && hub_only) ? (hub_sl < ns ? cps : 0u) : ns * cps);
     // thread 0: the open slow-list run of the current item (FINAL, recording)
     u32 seg_sl = 0xFFFFFFFFu, seg_start = 0;
     auto close_seg = [&]() {  // thread 0, after a barrier (every wave's slow stores of the item are done)
@@ -453,10 +457,11 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             lo = 0;
             hi = len = sg.len;
         } else {
-            sl = item / cps;
+            const bool hub = !FINAL && hub_only;
+            sl = hub ? hub_sl : item / cps;
             len = m->bk_cur[sl] < m->bk_cap[sl] ? m->bk_cur[sl] : m->bk_cap[sl];
             if (!FINAL) len = len * frac >> 16;
-            item_range(len, item % cps, cps, lo, hi);
+            item_range(len, hub ? item : item % cps, cps, lo, hi);
             src = bk + m->bk_base[sl];
         }
         if (lo >= hi) continue;

@@ -2033,6 +2033,9 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const bool slow2 = t.bucket_slow2 != 0;
     if (slow2 && (rc = grow(h->d_seg, h->seg_cap, (u64)ns * cps + 64, h->stream))) return rc;
     const u32 cps_seed = (u32)std::max<u64>(1, std::min<u64>(cps, (u64)((double)n * t.bucket_sample) / ((u64)ns << 16)));
+    // the first level streams only the hub's slice: one slice's sample, about 16K edges per part (one part per
+    // P2 block at most)
+    const u32 cps_hub = (u32)std::max<u64>(1, std::min<u64>(p2_blocks, (u64)((double)n * t.bucket_sample) / ns / 16384));
     const size_t f_lds = slice_filter_lds(), h_lds = bk::kSliceWords * sizeof(u32);
     const size_t vl_cur_off = offsetof(bk::Meta, vl_cur);
     u32 slot = 0;
@@ -2055,8 +2058,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     for (int l = 0; l < levels && !rc; ++l) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
         rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
-                      f_lds, h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps_seed, frac,
-                      slot++, h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err,
+                      f_lds, h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl,
+                      l == 0 ? cps_hub : cps_seed, frac, slot++, h->tune.drain_at, (u32)(l == 0), (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err,
                       (bk::SlowSeg*)nullptr);
         if (!rc)
             rc = launch_k(h, "seed_hook", 0, bk::slice_hook_kernel<false>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
@@ -2070,7 +2073,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
     rc = launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true>, dim3(p2_blocks), dim3(bk::kP2Block), f_lds,
                   h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps, 65536u, slot++,
-                  h->tune.drain_at, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr);
+                  h->tune.drain_at, 0u, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr);
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
                       h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
@@ -2087,7 +2090,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
         rc = launch_k(h, "slice_filter2", 0, bk::slice_filter_kernel<true, true>, dim3(p2_blocks), dim3(bk::kP2Block),
                       f_lds, h->d_parent, (const u64*)h->d_slow, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, 1u,
-                      65536u, slot++, h->tune.drain_at, (const u32*)giant, h->d_bk, slow_cap2, h->cap, h->d_err, h->d_seg);
+                      65536u, slot++, h->tune.drain_at, 0u, (const u32*)giant, h->d_bk, slow_cap2, h->cap, h->d_err, h->d_seg);
         if (!rc)
             rc = launch_k(h, "slice_hook2", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
                           h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
