@@ -1515,8 +1515,12 @@ struct FoldTune {
     bool bucket = true;
     u64 bucket_min_batch = 1ull << 25;
     u64 bucket_min_ids = (u64)kLdsBitmapMaxWords * 64 + 1;
-    int bucket_levels = 3;
-    double bucket_sample = 0.15;  // profiles/r2_sweep_c4_p1.log: 0.25 -> 0.15 = 12.74 -> 12.22 ms on C4
+    // since the first level streams only the hub's slice, the whole of it (C1 = every neighbour of h in the batch)
+    // + one level over a quarter of every bucket beat three levels over 15 % (profiles/r2c_sweep_seeding.log:
+    // C4 11.0 -> 10.8 ms, the share equal; round 2's first sweep, r2_sweep_c4_p1.log, predates the hub level)
+    int bucket_levels = 2;
+    double bucket_sample = 0.25;
+    double bucket_hub_sample = 1.0;  // the first level's share of the hub's bucket (C = {h}: one slice)
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
     int bucket_slow2 = 1;        // second filter level over the slow edges with C | N (C4's 1/8 share: 19 % slow edges)
     int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms)
@@ -2035,7 +2039,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u32 cps_seed = (u32)std::max<u64>(1, std::min<u64>(cps, (u64)((double)n * t.bucket_sample) / ((u64)ns << 16)));
     // the first level streams only the hub's slice: one slice's sample, about 16K edges per part (one part per
     // P2 block at most)
-    const u32 cps_hub = (u32)std::max<u64>(1, std::min<u64>(p2_blocks, (u64)((double)n * t.bucket_sample) / ns / 16384));
+    const u32 cps_hub = (u32)std::max<u64>(1, std::min<u64>(p2_blocks, (u64)((double)n * t.bucket_hub_sample) / ns / 16384));
+    const u32 frac_hub = (u32)std::max(0.0, std::min(65536.0, t.bucket_hub_sample * 65536.0));
     const size_t f_lds = slice_filter_lds(), h_lds = bk::kSliceWords * sizeof(u32);
     const size_t vl_cur_off = offsetof(bk::Meta, vl_cur);
     u32 slot = 0;
@@ -2059,7 +2064,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
         rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
                       f_lds, h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl,
-                      l == 0 ? cps_hub : cps_seed, frac, slot++, h->tune.drain_at, (u32)(l == 0), (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err,
+                      l == 0 ? cps_hub : cps_seed, l == 0 ? frac_hub : frac, slot++, h->tune.drain_at, (u32)(l == 0),
+                      (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err,
                       (bk::SlowSeg*)nullptr);
         if (!rc)
             rc = launch_k(h, "seed_hook", 0, bk::slice_hook_kernel<false>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
@@ -3158,6 +3164,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "bucket_min_ids") t.bucket_min_ids = (u64)value;
     else if (k == "bucket_levels") t.bucket_levels = std::max(0, std::min(6, (int)value));
     else if (k == "bucket_sample") t.bucket_sample = std::max(0.0, std::min(1.0, value));
+    else if (k == "bucket_hub_sample") t.bucket_hub_sample = std::max(0.0, std::min(1.0, value));
     else return set_err(GCC_E_INVALID, "unknown tuning key '%s'", key);
     return GCC_OK;
 }
