@@ -50,6 +50,7 @@ struct Meta {
     u32 spill;                   // 1: some edge fit neither its bucket nor the overflow list
     u32 gmin;                    // min C (seeding)
     u32 nseg;                    // FINAL P2: slow-list segments recorded (SlowSeg table)
+    u32 ring_used;               // FINAL P2 united some slow edges itself (its region was full): see bucket_join_kernel
     u32 slow_cnt[kMaxP2Blocks];  // FINAL P2: slow edges (source not in C) each block listed in its own region
 };
 
@@ -189,6 +190,7 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     block_prefix(m->vl_cap, m->vl_base, ns, s_scan);
     if (threadIdx.x < 16) m->work[threadIdx.x] = 0;
     if (threadIdx.x == 0) m->nseg = 0;
+    if (threadIdx.x == 0) m->ring_used = 0;
     if (threadIdx.x == 0) {
         m->ovf_cur = 0;
         m->spill = 0;
@@ -537,6 +539,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                         ++pos;
                     }
                 if (__ballot(spill_m != 0)) {  // past the region (never at the default sizes): united right here
+                    if (lane == 0) atomicOr(&m->ring_used, 1u);
 #pragma unroll
                     for (int k = 0; k < kP2Per; ++k)
                         ring_push((spill_m >> k) & 1u, ua[k], va[k], ring, wq, wd, parent, drain_at, 0xFFFFFFFFu);
@@ -701,6 +704,36 @@ __global__ __launch_bounds__(kBlock) void bucket_hook_kernel(u32* __restrict__ p
     }
 }
 
+// Deferred N (tune.bucket_defer): C |= N word by word, and N stays in nbits, UNSEEN in parent[], until the fold's
+// closing compress labels it g's root (compress_bits_kernel's newbits) — no per-id store — except the ids below g,
+// hooked here (each may become the component's root). Every later pass of
+// the fold treats an edge with one end in C | N as the hook of its other end (slow, rest), so nothing unions an
+// id of N directly; only FINAL P2's in-kernel ring unions (a full slow region, m->ring_used) could have made one
+// seen, and then every seen id of N is hooked under g here.
+__global__ __launch_bounds__(kBlock) void bucket_join_kernel(u32* __restrict__ parent, u32* __restrict__ bits,
+                                                             const u32* __restrict__ nbits, u32 nwords32,
+                                                             const u32* __restrict__ giant, const Meta* __restrict__ m) {
+    trace_start(kTrBkHook);
+    const u32 g = *giant;
+    const bool ring = m->ring_used != 0;
+    for (u64 w = (u64)blockIdx.x * kBlock + threadIdx.x; w < nwords32; w += (u64)gridDim.x * kBlock) {
+        u32 d = nbits[w];
+        if (!d) continue;
+        bits[w] |= d;
+        if (g == GCC_UNSEEN_DEV) continue;
+        // an id below g is hooked now: it becomes the component's root, which the compress must find
+        const u64 w0 = w * 32;
+        const u32 low = w0 >= g ? 0u : (w0 + 31 < g ? d : d & ((1u << (u32)(g - w0)) - 1u));
+        u32 todo = ring ? d : low;
+        while (todo) {
+            const u32 k = (u32)__builtin_ctz(todo);
+            todo &= todo - 1;
+            const u32 v = (u32)(w0 + k);
+            if (v < g || parent[v] != GCC_UNSEEN_DEV) hook_g(parent, g, v);
+        }
+    }
+}
+
 // The slow list (FINAL P2: edges whose source was not in C) against C | N: both ends in it -> already connected to
 // g; one end -> the other hooked under g; neither -> united. Block b takes part b % kSlowSplit of P2 block
 // (b / kSlowSplit)'s region, only up to that region's count (a grid-stride over every region's capacity read the
@@ -777,13 +810,25 @@ __global__ __launch_bounds__(kBlock) void bucket_init_kernel(u32* __restrict__ p
 
 // The overflow list (edges their bucket had no room for): united, skipped when both ends are in C. If the list
 // itself overflowed (spill), the WHOLE batch is united again: exact (union is idempotent), only slow.
+// An edge with one end in C | N (g's component) is the hook of its other end, and with both ends there nothing:
+// the overflow list and the whole-batch fallback take the slow kernel's rule, so they never union an id of C | N
+// directly (with the deferred N, such an id may still be UNSEEN: bucket_join_kernel).
+__device__ __forceinline__ void bucket_edge(u32* parent, const u32* bits, u32 g, u32 a, u32 b) {
+    NoCount c;
+    const u32 ia = lds_bit(bits, a), ib = lds_bit(bits, b);
+    if (ia & ib) return;
+    if (ia) hook_g(parent, g, b);
+    else if (ib) hook_g(parent, g, a);
+    else UF::unite(parent, a, b, c);
+}
+
 __global__ __launch_bounds__(kBlock) void bucket_rest_kernel(u32* __restrict__ parent, const u64* __restrict__ ovf,
                                                              u32 ovf_cap, const Meta* __restrict__ m,
                                                              const u32* __restrict__ bits,
                                                              const u64* __restrict__ edges, u64 n, u32 cap,
-                                                             u32* __restrict__ err) {
+                                                             u32* __restrict__ err, const u32* __restrict__ giant) {
     trace_start(kTrBkRest);
-    NoCount c;
+    const u32 g = *giant;
     const u64 stride = (u64)gridDim.x * kBlock;
     const u64 no = m->ovf_cur < ovf_cap ? m->ovf_cur : ovf_cap;
     for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < no; i += stride) {
@@ -793,15 +838,14 @@ __global__ __launch_bounds__(kBlock) void bucket_rest_kernel(u32* __restrict__ p
             flag_err(err, kErrOvf);
             continue;
         }
-        if (lds_bit(bits, a) & lds_bit(bits, b)) continue;
-        UF::unite(parent, a, b, c);
+        bucket_edge(parent, bits, g, a, b);
     }
     if (m->spill) {
         for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
             const u64 e = edges[i];
             u32 a = (u32)e, b = (u32)(e >> 32);
             if (!edge_ok(a, b, cap, err)) continue;
-            UF::unite(parent, a, b, c);
+            bucket_edge(parent, bits, g, a, b);
         }
     }
 }

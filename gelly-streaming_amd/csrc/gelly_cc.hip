@@ -1522,6 +1522,7 @@ struct FoldTune {
     double bucket_sample = 0.25;
     double bucket_hub_sample = 1.0;  // the first level's share of the hub's bucket (C = {h}: one slice)
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
+    int bucket_defer = 1;        // N labelled by the fold's closing compress instead of a store per id (bucket_join_kernel)
     int bucket_slow2 = 1;        // second filter level over the slow edges with C | N (C4's 1/8 share: 19 % slow edges)
     int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms)
 };
@@ -1576,6 +1577,8 @@ struct gcc_forest {
     u64* d_msg_oth = nullptr;  // encode scratch (gcc_forest_encode): per word, the seen ids outside the tracked component
     u64 version = 0;      // bumped by every mutation of parent[] (with host_valid = false)
     u64 enc_version = ~0ull;  // `version` when d_msg_oth was written: equal = the masks still describe parent[]
+    u64 mask_version = ~0ull;  // `version` when a compress last wrote the others' masks into d_msg_oth
+    bool deferred_n = false;   // the bucketed fold left N in d_nbits for its closing compress
     bool witness_armed = false;  // the last encode already reset d_witness (stream-ordered before the next absorb)
 
     unsigned long long* d_counts = nullptr;
@@ -2002,6 +2005,15 @@ static int grow(T*& p, u64& cap, u64 need, hipStream_t st) {
     return GCC_OK;
 }
 
+// encode scratch (msg kernels): per 64-id word the others' mask, then per count block its count and list base
+static u32 msg_blocks(const gcc_forest* h) { return (u32)((((u64)h->cap + 63) / 64 + kMsgWordsPerBlock - 1) / kMsgWordsPerBlock); }
+static int ensure_msg_scratch(gcc_forest* h) {
+    if (h->d_msg_oth) return GCC_OK;
+    const u64 nw = ((u64)h->cap + 63) / 64;
+    HIP_TRY(hipMalloc((void**)&h->d_msg_oth, nw * sizeof(u64) + 2 * (size_t)msg_blocks(h) * sizeof(u32)));
+    return GCC_OK;
+}
+
 static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const FoldTune& t = h->tune;
     h->rec_all = false;
@@ -2083,9 +2095,12 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
                       h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
+    const bool defer = t.bucket_defer != 0;
     if (!rc)
-        rc = launch_k(h, "bucket_hook", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
-                      h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
+        rc = defer ? launch_k(h, "bucket_join", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
+                              h->d_parent, bits, (const u32*)h->d_nbits, nw32, (const u32*)giant, (const bk::Meta*)h->d_meta)
+                   : launch_k(h, "bucket_hook", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
+                              h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
     // Second level over the slow edges, now against C | N: a slow edge whose source joined N is a hook of its
     // target (its v-list again), only the rest stays slow. Its input is FINAL P2's slow runs (one source slice
     // each); its slow edges go to the bucket storage, which P2 has consumed.
@@ -2101,8 +2116,11 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
             rc = launch_k(h, "slice_hook2", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
                           h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
         if (!rc)
-            rc = launch_k(h, "bucket_hook2", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
-                          h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
+            rc = defer ? launch_k(h, "bucket_join2", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock),
+                                  0, h->d_parent, bits, (const u32*)h->d_nbits, nw32, (const u32*)giant,
+                                  (const bk::Meta*)h->d_meta)
+                       : launch_k(h, "bucket_hook2", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock),
+                                  0, h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
         slow_list = h->d_bk;
         slow_list_cap = slow_cap2;
     }
@@ -2113,8 +2131,9 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (!rc)
         rc = launch_k(h, "bucket_rest", 0, bk::bucket_rest_kernel, dim3(grid_for(n / 64 + 1, kMaxGrid)), dim3(kBlock), 0,
                       h->d_parent, (const u64*)h->d_ovf, ovf_cap, (const bk::Meta*)h->d_meta, (const u32*)bits, edges, n,
-                      h->cap, h->d_err);
+                      h->cap, h->d_err, (const u32*)giant);
     if (rc) return rc;
+    h->deferred_n = defer;
     h->pending_reset = false;
     h->has_giant = true;
     if (bucket_stats()) {  // diagnostics: the lists' fill (synchronises)
@@ -2165,6 +2184,15 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
             h->last_fold_last = (int)h->kev_used - 1;
         }
         mark_mutated(h);
+        if (h->deferred_n) {  // the closing compress labels N (and writes the others' masks for a merge's encode)
+            h->deferred_n = false;
+            rc = ensure_msg_scratch(h);
+            bool masks = false;
+            if (!rc) rc = compress_now(h, "compress", h->d_msg_oth, &masks, reinterpret_cast<const u64*>(h->d_nbits));
+            if (rc) return rc;
+            HIP_TRY(hipMemsetAsync(h->d_nbits, 0, (size_t)2 * (h->nwords() + (h->nwords() & 1)) * sizeof(u32), h->stream));
+            if (masks) h->mask_version = h->version;
+        }
         return GCC_OK;
     }
     if (seeded) {
@@ -2841,9 +2869,7 @@ int gcc_forest_encode(gcc_forest* h, void* d_msg, uint64_t cap_others) {
     u32* others = reinterpret_cast<u32*>(bits + nw);
     const u32 nb = (u32)((nw + kMsgWordsPerBlock - 1) / kMsgWordsPerBlock);
     if (!h->d_witness) HIP_TRY(hipMalloc((void**)&h->d_witness, kMaxPeers * sizeof(u32)));
-    if (!h->d_msg_oth) {  // encode scratch: the others' masks, then per count block its count and list base
-        HIP_TRY(hipMalloc((void**)&h->d_msg_oth, nw * sizeof(u64) + 2 * (size_t)nb * sizeof(u32)));
-    }
+    if ((rc = ensure_msg_scratch(h))) return rc;
     u32* cnt = reinterpret_cast<u32*>(h->d_msg_oth + nw);
     u32* base = cnt + nb;
     // An uncompressed forest is compressed first, by a compress that also writes the others' masks (one pass
@@ -2855,6 +2881,8 @@ int gcc_forest_encode(gcc_forest* h, void* d_msg, uint64_t cap_others) {
     if (!h->compressed && h->filter_enabled()) {
         rc = compress_now(h, "compress", h->d_msg_oth, &masks);
         if (rc) return rc;
+    } else if (h->compressed && h->mask_version == h->version) {
+        masks = true;  // the last compress (a bucketed fold's closing one) wrote them and nothing changed since
     }
     const bool find = !h->compressed;
     const bool track = h->has_giant && h->d_bits && h->d_giant;
@@ -3159,6 +3187,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = (int)value == 1 ? 1 : 0;
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
+    else if (k == "bucket_defer") t.bucket_defer = value != 0.0;
     else if (k == "bucket") t.bucket = value != 0;
     else if (k == "bucket_min_batch") t.bucket_min_batch = (u64)value;
     else if (k == "bucket_min_ids") t.bucket_min_ids = (u64)value;

@@ -55,7 +55,8 @@ def mismatch(got, want):
 @pytest.mark.parametrize("knobs", [{}, {"bucket_levels": 0}, {"bucket_levels": 1, "bucket_sample": 1.0},
                                    {"bucket_sample": 0.0}, {"bucket_levels": 6, "bucket_sample": 0.05},
                                    {"bucket_slow2": 0}, {"bucket_levels": 0, "bucket_slow2": 0},
-                                   {"bucket_hub_sample": 0.0}, {"bucket_levels": 3, "bucket_hub_sample": 0.15}])
+                                   {"bucket_hub_sample": 0.0}, {"bucket_levels": 3, "bucket_hub_sample": 0.15},
+                                   {"bucket_defer": 0}, {"bucket_defer": 0, "bucket_slow2": 0}])
 def test_bucketed_fold_rmat(torch_cuda, knobs):
     """R-MAT s20, 2^22 edges, one fresh batch through the bucketed fold (seeding knobs vary the sample and the
     level count: the result may not depend on them)."""

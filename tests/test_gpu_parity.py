@@ -530,6 +530,7 @@ KNOB_CASES = {
     "pin_chunk": {"pin_chunk": 4096},
     "bucket_p1": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 0},
     "bucket_slow2": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_slow2": 0},
+    "bucket_defer": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_defer": 0},
     "bucket_hub_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_hub_sample": 0.1},
     "lds_edges_per_word": {"lds_edges_per_word": 1e9},  # the short windows take the global-bitmap filter
 }
