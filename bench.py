@@ -104,18 +104,40 @@ def rank_chunks(starts, rank, world):
     return out
 
 
-def profile_record(workload):
-    """The newest committed rocprofv3 PMC summary for this workload (profiles/*_pmc_<workload>.json), or None."""
+def pmc_kernel_match(label, kname):
+    """Does a rocprof kernel name belong to bench's kernel label? 'slice_filter_kernel<true>' matches
+    'void bk::slice_filter_kernel<true, false>(...)' (the label's template arguments are a prefix of the name's)."""
+    base, _, targs = label.partition("<")
+    at = kname.find(base + "<") if targs else kname.find(base + "(")
+    if at < 0:
+        at = kname.find(base)
+        return at >= 0 and not targs
+    if not targs:
+        return True
+    got = kname[at + len(base) + 1:].split(">")[0].replace(" ", "")
+    return got.startswith(targs.rstrip(">").replace(" ", ""))
+
+
+def profile_record(workload, kernel=None, units=None):
+    """The newest committed rocprofv3 PMC summary for this workload (profiles/*_pmc_<workload>*.json) whose kernel is
+    `kernel` and whose units per launch match `units` (within 1 %), or None."""
     pdir = os.path.join(ROOT, "profiles")
-    best = None
-    if os.path.isdir(pdir):
-        for f in sorted(os.listdir(pdir)):
-            if f.endswith(f"_pmc_{workload}.json"):
-                try:
-                    best = json.load(open(os.path.join(pdir, f)))
-                except Exception:
-                    continue
-    return best
+    if not os.path.isdir(pdir):
+        return None
+    for f in sorted(os.listdir(pdir), reverse=True):
+        if f"_pmc_{workload}" not in f or not f.endswith(".json"):
+            continue
+        try:
+            rec = json.load(open(os.path.join(pdir, f)))
+        except Exception:
+            continue
+        if kernel and not pmc_kernel_match(kernel, rec.get("kernel", "")):
+            continue
+        if units is not None and abs(rec.get("edges_per_launch", 0) - units) > 0.01 * max(1, units):
+            continue
+        rec["file"] = f"profiles/{f}"
+        return rec
+    return None
 
 
 def cpu_quota():
@@ -208,13 +230,10 @@ def kernel_stats(log, V, inst_steps):
 
 def make_roofline(kstats, phases, spans, inst_steps, workload, timing_note, host_fold_s):
     dominant = max(kstats, key=lambda k: kstats[k]["ms_per_step"]) if kstats else None
-    prof = profile_record(workload)
     dom = kstats.get(dominant, {})
+    prof = profile_record(workload, dominant, dom.get("units_avg", 0)) if dominant else None
     achieved = dom.get("achieved_gbs")
-    traffic = None
-    if prof and dominant and dominant in prof.get("kernel", "") and \
-            abs(prof.get("edges_per_launch", 0) - dom.get("units_avg", 0)) <= 0.01 * max(1, dom.get("units_avg", 0)):
-        traffic = prof["hbm_bytes_per_launch"]
+    traffic = prof["hbm_bytes_per_launch"] if prof else None
     avg_fold_s = (sum(ms for ms, _ in spans) / len(spans) / 1e3) if spans else None
     avg_fold_edges = (sum(n for _, n in spans) / len(spans)) if spans else None
     pipeline_gbs = BYTES_PER_EDGE * avg_fold_edges / avg_fold_s / 1e9 if spans and avg_fold_s else None
@@ -222,8 +241,8 @@ def make_roofline(kstats, phases, spans, inst_steps, workload, timing_note, host
         "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
         "traffic": traffic, "traffic_unit": "bytes per launch",
-        "traffic_source": (prof["source"] + (f"; L2 hit rate {prof['l2_hit_rate']:.2f}" if "l2_hit_rate" in prof else ""))
-        if traffic else None,
+        "traffic_source": (prof["source"] + (f"; L2 hit rate {prof['l2_hit_rate']:.2f}" if "l2_hit_rate" in prof else "")
+                           + f"; {prof['file']}") if traffic else None,
         "kernel_ms_avg": dom.get("ms_avg"), "kernel_units_per_launch": int(dom.get("units_avg", 0)),
         "bytes_per_unit": KERNEL_BYTES.get(dominant), "timing": timing_note, "kernels": kstats,
         "phases_ms_per_step": {k: sum(v) / max(1, inst_steps) for k, v in phases.items()},

@@ -1508,7 +1508,10 @@ struct FoldTune {
     bool incremental = true;
     bool inc_inplace = true;  // the incremental compress rewrites only changed parent[] slots (no spare buffer)
     u64 inc_min_ids = 1ull << 22;
-    u64 inc_div = 8;
+    // 64, not 8 (round 2): a batch of 1/16 of the ids (C3's last 1M-edge window, ~500K hooks) fills the 1M-bit bloom
+    // to a ~60 % false-hit rate, so the incremental compress walks for most ids anyway; and in two full-suite runs
+    // that window's incremental compress left ONE label stale (not root-caused). C5 (1/256) keeps it.
+    u64 inc_div = 64;
     // bucketed fold of a fresh forest (bucket_fold.h): batches of >= bucket_min_batch edges over >= bucket_min_ids
     // ids (default: exactly the forests whose giant bitmap does not fit LDS); seeding = bucket_levels P2 + P3 levels
     // over the first bucket_sample of every bucket

@@ -165,16 +165,26 @@ def test_stream_fixture_device_resident(golden, torch_cuda, name):
 
 
 # ---- full-size configs vs the oracle, per window ----
-def run_device_windows(torch_cuda, cfg, starts, V):
+def run_device_windows(torch_cuda, cfg, starts, V, knobs=None, raw=None):
     d = device_stream(torch_cuda, cfg)
     ds = DisjointSet(V)
+    if knobs:
+        ds.tune(**knobs)
     out = []
     for w in range(len(starts) - 1):
         b, e = int(starts[w]), int(starts[w + 1])
         ds.fold_device(d.data_ptr() + 8 * b, e - b)
+        if raw is not None:  # diagnostics: the forest before the window's emission (no compress)
+            raw.append(ds.raw_parent())
         out.append(ds.labels().copy())
     ds.close()
     return out
+
+
+def _host_root(par, v):
+    while par[v] < v:
+        v = int(par[v])
+    return v
 
 
 @pytest.mark.parametrize("cfg_name,window", [("c2_rmat20", 1 << 20), ("c2_rmat20", 1 << 24), ("c3_gnm24", 1 << 22)])
@@ -184,9 +194,19 @@ def test_full_config_parity(torch_cuda, cfg_name, window):
     starts = np.asarray(list(range(0, E, window)) + [E], dtype=np.uint64)
     pairs = G.generate_host(cfg)
     want = orc.cc_stream(pairs, starts, V, partitions=4, threads=4)
-    got = run_device_windows(torch_cuda, cfg, starts, V)
+    raw = []
+    got = run_device_windows(torch_cuda, cfg, starts, V, raw=raw)
     for w, lab in enumerate(got):
-        assert orc.label_digest(lab) == int(want["digest"][w]), (cfg_name, w)
+        if orc.label_digest(lab) != int(want["digest"][w]):  # diagnostics: the same windows with every
+            # incremental compress off (full compresses only), to tell which stage a mismatch comes from
+            ref = run_device_windows(torch_cuda, cfg, starts, V, knobs={"incremental": 0})
+            bad = np.flatnonzero(lab != ref[w])
+            walk = [(int(v), _host_root(raw[w], int(v)), int(raw[w][v])) for v in bad[:4]]
+            prev = [(int(v), int(got[w - 1][v]) if w else -1) for v in bad[:4]]
+            pytest.fail(f"{cfg_name} window {w}: digest mismatch; raw-forest walks (v, root, parent) {walk}; "
+                        f"previous labels {prev}; vs the full-compress forest {bad.size} labels differ"
+                        f"{'' if bad.size == 0 else f' (first at {int(bad[0])}: {int(lab[bad[0]])} vs {int(ref[w][bad[0]])})'}"
+                        f", full-compress forest digest {'matches' if orc.label_digest(ref[w]) == int(want['digest'][w]) else 'differs'}")
         seen = lab != UNSEEN
         assert int(seen.sum()) == int(want["seen"][w])
         assert int(np.count_nonzero(lab[seen] == np.flatnonzero(seen))) == int(want["components"][w])
