@@ -408,8 +408,10 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
 
 // Merge: into ∪ {(v, labels[v])}. labels may be any parent array of a forest over the same id range
 // (compressed or not) — its (key, parent) pairs generate its partition (DisjointSet.merge :132-136).
+// A label array comes from outside (another forest, rank or device: gcc_forest_merge_labels_device), so a label
+// is validated like a device batch's ids: one >= cap is skipped (never dereferenced) and *err is set.
 __global__ __launch_bounds__(kBlock) void merge_labels_kernel(u32* __restrict__ parent, const u32* __restrict__ labels,
-                                                              u32 n) {
+                                                              u32 n, u32 cap, u32* __restrict__ err) {
     trace_start(kTrMergeLabels);
     NoCount c;
     const u64 stride = (u64)gridDim.x * kBlock;
@@ -417,6 +419,10 @@ __global__ __launch_bounds__(kBlock) void merge_labels_kernel(u32* __restrict__ 
         const u32 v = (u32)vv;
         const u32 l = labels[v];
         if (l == UNSEEN) continue;
+        if (l >= cap) {
+            *err = 1u;
+            continue;
+        }
         UF::unite(parent, v, l, c);
     }
 }
@@ -1679,6 +1685,16 @@ static bool sync_each_launch() {
     return on;
 }
 
+// GELLY_SYNC_EACH for the merge-message kernels (launched directly, not through launch_k)
+static int msg_launched(gcc_forest* h, const char* name) {
+    HIP_TRY(hipGetLastError());
+    if (sync_each_launch()) {
+        const hipError_t e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return set_err(GCC_E_HIP, "kernel %s: %s", name, hipGetErrorString(e));
+    }
+    return GCC_OK;
+}
+
 template <typename F, typename... Args>
 static int launch_k(gcc_forest* h, const char* name, u64 edges, F kernel, dim3 grid, dim3 block, size_t shmem,
                     Args... args) {
@@ -2794,7 +2810,7 @@ int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, u
     if (rc) return rc;
     if (n == 0) return GCC_OK;
     hipLaunchKernelGGL(merge_labels_kernel, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, into->stream, into->d_parent,
-                       d_labels, n);
+                       d_labels, n, into->cap, into->d_err);
     HIP_TRY(hipGetLastError());
     into->host_valid = false;
     ++into->version;
@@ -2892,25 +2908,37 @@ int gcc_forest_encode(gcc_forest* h, void* d_msg, uint64_t cap_others) {
     hipLaunchKernelGGL(msg_header_kernel, dim3(1), dim3(kMaxPeers), 0, h->stream, hdr,
                        h->d_giant ? h->d_giant + h->giant_slot : hdr, h->has_giant ? 1u : 0u, h->cap, h->d_witness,
                        (const u32*)h->d_parent, track ? h->d_giant + (h->giant_slot ^ 1) : nullptr);
+    if ((rc = msg_launched(h, "msg_header_kernel"))) return rc;
     h->witness_armed = true;
     u64* mine = track ? h->d_bits : nullptr;
     const u32* gprev = track ? (const u32*)(h->d_giant + h->giant_slot) : nullptr;
-    if (masks && track)
+    if (masks && track) {
         hipLaunchKernelGGL(msg_cnt_kernel, dim3(nb), dim3(kBlock), 0, h->stream, (const u64*)h->d_msg_oth,
                            (const u64*)h->d_bits, bits, nw, cnt);
-    else if (find)
+        if ((rc = msg_launched(h, "msg_cnt_kernel"))) return rc;
+    }
+    else if (find) {
         hipLaunchKernelGGL(msg_count_kernel<true>, dim3(nb), dim3(kMsgBlock), 0, h->stream, (const u32*)h->d_parent,
                            h->cap, (const u32*)hdr, gprev, bits, mine, h->d_msg_oth, cnt);
-    else
+        if ((rc = msg_launched(h, "msg_count_kernel"))) return rc;
+    }
+    else {
         hipLaunchKernelGGL(msg_count_kernel<false>, dim3(nb), dim3(kMsgBlock), 0, h->stream, (const u32*)h->d_parent,
                            h->cap, (const u32*)hdr, gprev, bits, mine, h->d_msg_oth, cnt);
+        if ((rc = msg_launched(h, "msg_count_kernel"))) return rc;
+    }
     hipLaunchKernelGGL(msg_scan_kernel, dim3(1), dim3(kScanBlock), 0, h->stream, (const u32*)cnt, nb, base, hdr);
-    if (find)
+    if ((rc = msg_launched(h, "msg_scan_kernel"))) return rc;
+    if (find) {
         hipLaunchKernelGGL(msg_write_kernel<true>, dim3(nb), dim3(kBlock), 0, h->stream, (const u32*)h->d_parent, h->cap,
                            (const u64*)h->d_msg_oth, (const u32*)base, (const u32*)hdr, gprev, others, (u64)cap_others);
-    else
+        if ((rc = msg_launched(h, "msg_write_kernel"))) return rc;
+    }
+    else {
         hipLaunchKernelGGL(msg_write_kernel<false>, dim3(nb), dim3(kBlock), 0, h->stream, (const u32*)h->d_parent, h->cap,
                            (const u64*)h->d_msg_oth, (const u32*)base, (const u32*)hdr, gprev, others, (u64)cap_others);
+        if ((rc = msg_launched(h, "msg_write_kernel"))) return rc;
+    }
     HIP_TRY(hipGetLastError());
     if (track) h->giant_slot ^= 1;  // the header kernel stored the tracked component's current root there
     h->enc_version = h->version;
@@ -2937,6 +2965,7 @@ int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_by
         h->witness_armed = false;
         hipLaunchKernelGGL(msg_overlap_kernel, dim3(grid_for((u64)count * ((nw + 63) / 64) * 64, kMaxGrid)), dim3(kBlock),
                            0, h->stream, msgs, (u64)stride_bytes, count, skip, h->cap, mine, h->d_witness);
+        if ((rc = msg_launched(h, "msg_overlap_kernel"))) return rc;
     }
     // one list entry per lane; with no tracked component every giant goes id by id too (one word per wave)
     const u64 lists = std::max<u64>((u64)count * cap_others, 1);
@@ -2948,13 +2977,16 @@ int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_by
     const bool masks = tracked && h->d_msg_oth && h->enc_version == h->version;
     u64* newbits = (masks && h->filter_enabled()) ? h->d_msg_oth : nullptr;
     const u32* troot = tracked ? (const u32*)(h->d_giant + h->giant_slot) : nullptr;
-    if (tracked)
+    if (tracked) {
         hipLaunchKernelGGL(msg_absorb_bits_kernel, dim3(grid_for(nw * 64, kMaxGrid)), dim3(kBlock), 0, h->stream,
                            h->d_parent, msgs, (u64)stride_bytes, count, skip, h->cap, mine, troot,
                            (const u32*)h->d_witness, masks ? (const u64*)h->d_msg_oth : nullptr, newbits);
+        if ((rc = msg_launched(h, "msg_absorb_bits_kernel"))) return rc;
+    }
     hipLaunchKernelGGL(msg_absorb_kernel, dim3(grid_for(work, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent, msgs,
                        (u64)stride_bytes, count, skip, (u64)cap_others, h->cap, tracked,
                        tracked ? (const u32*)h->d_witness : nullptr, (const u64*)newbits, troot);
+    if ((rc = msg_launched(h, "msg_absorb_kernel"))) return rc;
     HIP_TRY(hipGetLastError());
     mark_mutated(h);
     if (newbits) return compress_now(h, "compress", nullptr, nullptr, newbits);

@@ -307,8 +307,14 @@ class ForestGroup:
                 buf = forest.exchange_tensor()  # compress swaps buffers: fetch the current labels every round
                 partner = self._global(self.rank ^ step)
                 ops = [dist.P2POp(dist.isend, buf, partner, self.group), dist.P2POp(dist.irecv, recv, partner, self.group)]
+                if self._gloo_cuda(buf):  # gloo's P2P on CUDA tensors is not ordered with the stream: fence both sides
+                    import torch
+
+                    torch.cuda.synchronize(buf.device)
                 for req in dist.batch_isend_irecv(ops):
                     req.wait()
+                if self._gloo_cuda(buf):
+                    torch.cuda.synchronize(buf.device)
                 forest.absorb(recv)
                 forest.compress()
                 step <<= 1
@@ -320,6 +326,10 @@ class ForestGroup:
                 if p != self.rank:
                     forest.absorb(t)
             forest.compress()
+
+    def _gloo_cuda(self, t) -> bool:
+        """A CUDA tensor over the gloo backend (one-GPU rehearsals of the N > 1 path)."""
+        return t.device.type == "cuda" and self._dist.get_backend(self.group) == "gloo"
 
     def reduce(self, summary, combineFun=None):
         """SummaryBulkAggregation's timeWindowAll(...).reduce(combineFun) across ranks, for a forest summary."""
