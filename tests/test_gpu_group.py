@@ -229,3 +229,27 @@ def test_group_merge_deferred_new_ids():
     finally:
         for ds in forests:
             ds.close()
+
+
+def test_merge_labels_rejects_out_of_range_labels():
+    """A received label array is untrusted input (gcc_forest_merge_labels_device): a label >= id_capacity is skipped
+    (never dereferenced) and reported once by the next synchronising call; the other labels are merged."""
+    import torch
+
+    from gelly_stream import DisjointSet
+    from gelly_stream.native import GellyCCError
+
+    V = 1 << 16
+    lab = np.full(V, 0xFFFFFFFF, dtype=np.uint32)
+    lab[10:20] = 10          # {10..19}
+    lab[30] = V + 7          # out of range
+    lab[31] = 0xFFFFFFF0     # out of range
+    d = torch.from_numpy(lab.view(np.int32)).cuda()
+    with DisjointSet(V) as ds:
+        ds.merge_labels_device(d.data_ptr(), V)
+        with pytest.raises(GellyCCError, match="id_capacity"):
+            ds.labels()
+        got = ds.labels()
+        want = np.full(V, 0xFFFFFFFF, dtype=np.uint32)
+        want[10:20] = 10
+        assert np.array_equal(got, want)
