@@ -2235,14 +2235,25 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
             rc = launch_plain(h, d_pairs + 2 * b, e - b, "sample");
             b = e;
         }
-        if (!rc && b < n) rc = refresh_now(h);
         if (!rc && b < n && t.filter_min_share > 0) {
             // once per forest: is the voted component a giant among the seen samples? If not, the filter would
-            // send almost every edge down its slow path, and the plain fold is faster (C3, C5)
+            // send almost every edge down its slow path, and the plain fold is faster (C3, C5). The vote alone
+            // answers that; the bitmap refresh only runs when the filter stays on (C3: 1.135 -> 1.107 ms).
+            rc = alloc_filter(h);
+            if (!rc && !h->has_giant)
+                rc = launch_k(h, "vote", 0, giant_vote_kernel, dim3(1), dim3(1024), 0, h->d_parent, h->cap,
+                              h->d_giant + h->giant_slot, h->d_giant + 4);
+            if (rc) return rc;
+            h->has_giant = true;
             u32 share[2] = {0, 0};
             HIP_TRY(hipMemcpyAsync(share, h->d_giant + 4, sizeof(share), hipMemcpyDeviceToHost, h->stream));
             HIP_TRY(hipStreamSynchronize(h->stream));
             h->filter_off = share[0] < t.filter_min_share * share[1];
+            if (!h->filter_off) rc = refresh_now(h);
+            else  // no refresh: the tracked-component bitmap is the empty set (valid: components only grow)
+                HIP_TRY(hipMemsetAsync(h->d_bits, 0, (size_t)h->nwords() * sizeof(u64), h->stream));
+        } else if (!rc && b < n) {
+            rc = refresh_now(h);
         }
         if (!rc && b < n && h->filter_off) {
             rc = launch_plain(h, d_pairs + 2 * b, n - b, "plain");
