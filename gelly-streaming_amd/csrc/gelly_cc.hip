@@ -1738,7 +1738,7 @@ static int stream_sync_checked(gcc_forest* h) {
             return set_err(GCC_E_INTERNAL, "bucketed fold consistency check failed (flags 0x%x: %s%s%s%s)", e,
                            (e & bk::kErrP2) ? "P2 bucket entry " : "", "",
                            (e & bk::kErrSlow) ? "slow-list entry " : "", (e & bk::kErrOvf) ? "overflow entry" : "");
-        return set_err(GCC_E_INVALID, "a device batch held a vertex id >= id_capacity %u (those edges were skipped)",
+        return set_err(GCC_E_INVALID, "a device batch or label array held an id >= id_capacity %u (those entries were skipped)",
                        h->cap);
     }
     return GCC_OK;

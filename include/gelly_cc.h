@@ -123,7 +123,8 @@ int gcc_forest_sync(gcc_forest* h);  /* flush + wait for the handle's stream */
 /* ---- combine: CombineCC.reduce / DisjointSet.merge (ConnectedComponents.java:116-125, DisjointSet.java:132-136) ---- */
 int gcc_forest_merge(gcc_forest* into, gcc_forest* from); /* into := into ∪ from (any two devices) */
 /* into := into ∪ {(v, labels[v]) : labels[v] != GCC_UNSEEN}; d_labels: n u32 in HBM of into's device,
- * ordered on into's stream (the receive side of the cross-GPU merge) */
+ * ordered on into's stream (the receive side of the cross-GPU merge). A label >= id_capacity is skipped (never
+ * dereferenced) and reported by the next synchronising call as GCC_E_INVALID, like an id of a device batch */
 int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, uint32_t n);
 
 /* ---- cross-GPU merge message: the partial forest as the RCCL payload (replaces the Kryo-serialised
