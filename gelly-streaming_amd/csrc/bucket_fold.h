@@ -64,6 +64,36 @@ struct SlowSeg {
 
 __device__ __forceinline__ u32 lds_bit(const u32* s, u32 x) { return (s[x >> 5] >> (x & 31)) & 1u; }
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+typedef uint16_t u16;
+typedef u16 u16x4 __attribute__((ext_vector_type(4)));
+
+// ---- bucket entries: 6 bytes (round 3; round 2 stored the u64 edge). The bucket (= source slice s) already names
+// the source's high bits, so an entry holds the target v (< 2^27: ns <= 256 slices of 2^19 ids) and the source's
+// 19 slice-local bits ul, in two parallel arrays of the same index: lo (u32) = v | ul[4:0] << 27, hi (u16) =
+// ul[18:5]. hi = 0xFFFF (ul never reaches 2^19) marks a padding slot or an unused chunk tail. P1 writes and P2 reads
+// 6 B per edge instead of 8: 25 % of both passes' bucket traffic.
+constexpr u32 kTgtBits = 27;
+constexpr u32 kTgtMask = (1u << kTgtBits) - 1;
+constexpr u16 kPadHi = 0xFFFF;
+
+// e = (v << 32) | u, or ~0 (padding)
+__device__ __forceinline__ u32 bk_lo_of(u64 e) {
+    return e == ~0ull ? 0xFFFFFFFFu : (u32)(e >> 32) | (((u32)e & (kSliceIds - 1)) << kTgtBits);
+}
+__device__ __forceinline__ u16 bk_hi_of(u64 e) {
+    return e == ~0ull ? kPadHi : (u16)(((u32)e & (kSliceIds - 1)) >> (32 - kTgtBits));
+}
+
+// the source (slice base sbase | ul) and target of an entry; false for padding
+__device__ __forceinline__ bool bk_decode(u32 lo, u16 hi, u32 sbase, u32& u, u32& v) {
+    u = sbase | ((u32)hi << (32 - kTgtBits)) | (lo >> kTgtBits);
+    v = lo & kTgtMask;
+    return hi != kPadHi;
+}
+
+// the bucket storage of S entries (S a multiple of 16): lo at the start, hi right after (16-B aligned)
+__host__ __device__ inline u64 bk_entries(u64 storage) { return (storage + 15) / 16 * 16; }
+__host__ __device__ inline u64 bk_bytes(u64 storage) { return 6 * bk_entries(storage); }
 
 // Internal consistency checks: every id a kernel takes from an internal list (buckets, slow and overflow lists) and
 // uses to index GLOBAL memory must be < cap. It always is; if one were not, the entry is skipped (never
@@ -231,15 +261,16 @@ __device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u
 // order and writes every run out contiguously (runs of ~kP1Tile / ns edges). The next tile's loads are in flight
 // meanwhile. Bad ids: skipped + *err. The odd last edge of an odd-length batch and every edge past its bucket's
 // capacity go to the overflow list.
-// P1's dynamic LDS: the tile in bucket order, every bucket's run padded to an even length — up to one slot per
+// P1's dynamic LDS: the tile in bucket order, every bucket's run padded to a multiple of 4 — up to three slots per
 // slice beyond the tile. (Round 2 first sized it to the tile alone: a full tile's last padded slots fell past the
 // allocation and relied on the LDS allocation's rounding slack; a 1024 x 8 geometry with less slack lost edges.)
-constexpr size_t p1_lds(int block, int per) { return ((size_t)block * per + kMaxSlicesLds) * sizeof(u64); }
+constexpr size_t p1_lds(int block, int per) { return ((size_t)block * per + 3 * kMaxSlicesLds) * sizeof(u64); }
 
 template <int P1B, int P1P>
 __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
-                                                          Meta* __restrict__ m, u64* __restrict__ bk,
-                                                          u64* __restrict__ ovf, u32 ovf_cap, u32* __restrict__ err) {
+                                                          Meta* __restrict__ m, u32* __restrict__ bk_lo,
+                                                          u16* __restrict__ bk_hi, u64* __restrict__ ovf, u32 ovf_cap,
+                                                          u32* __restrict__ err) {
     trace_start(kTrBkP1);
     // the tile in bucket order: dynamic LDS (p1_lds: P1B * P1P + kMaxSlicesLds u64, 66 / 130 KiB), set up like every
     // kernel's LDS beyond 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-slice state below is static
@@ -304,39 +335,45 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
             if (ok[k]) rk[k] = atomicAdd(&s_cnt[ua[k] >> kSliceBits], 1u);
         }
         __syncthreads();  // the tile's counts are complete
-        // every bucket's run is padded to an even length with one ~0 entry (P2 skips it), so that runs, tile
-        // slots and list positions stay even and the write-out moves a pair of edges per 16-B store
-        for (u32 s = threadIdx.x; s < ns; s += P1B) s_pc[s] = (s_cnt[s] + 1) & ~1u;
+        // every bucket's run is padded to a multiple of 4 with ~0 entries (P2 skips them), so that runs, tile
+        // slots and list positions stay multiples of 4 and the write-out moves 4 entries per lane (16 B of lo, 8 of hi)
+        for (u32 s = threadIdx.x; s < ns; s += P1B) s_pc[s] = (s_cnt[s] + 3) & ~3u;
         __syncthreads();
         count_scan<P1B>(s_pc, s_start, ns, s_wsum);
         for (u32 s = threadIdx.x; s < ns; s += P1B) {
             if (s_pc[s]) reserve_run(runs, s, s_pc[s], &m->bk_cur[s], s_cap[s]);
-            if (s_cnt[s] & 1) s_srt[s_start[s] + s_cnt[s]] = ~0ull;
+            for (u32 j = s_cnt[s]; j < s_pc[s]; ++j) s_srt[s_start[s] + j] = ~0ull;
         }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < P1P; ++k)
             if (ok[k]) s_srt[s_start[ua[k] >> kSliceBits] + rk[k]] = ((u64)va[k] << 32) | ua[k];
         __syncthreads();
-        const u32 tot2 = (s_start[ns - 1] + s_pc[ns - 1]) / 2;
-        for (u32 x2 = threadIdx.x; x2 < tot2; x2 += P1B) {
-            const u64x2 e = reinterpret_cast<const u64x2*>(s_srt)[x2];  // slot 2 x2 is never padding
-            const u32 s = (u32)e.x >> kSliceBits;
-            const u32 off = run_pos(runs, s, 2 * x2 - s_start[s]);     // even: both slots in one chunk
+        const u32 tot4 = (s_start[ns - 1] + s_pc[ns - 1]) / 4;
+        for (u32 x4 = threadIdx.x; x4 < tot4; x4 += P1B) {
+            const u64x2 ea = reinterpret_cast<const u64x2*>(s_srt)[2 * x4];      // slot 4 x4 is never padding
+            const u64x2 eb = reinterpret_cast<const u64x2*>(s_srt)[2 * x4 + 1];
+            const u64 e[4] = {ea.x, ea.y, eb.x, eb.y};
+            const u32 s = (u32)e[0] >> kSliceBits;
+            const u32 off = run_pos(runs, s, 4 * x4 - s_start[s]);  // a multiple of 4: all four in one chunk
             if (off != 0xFFFFFFFFu) {
-                *reinterpret_cast<u64x2*>(bk + s_base[s] + off) = e;   // 16-B aligned (bases: 16-entry multiples)
+                const u4 lo = {bk_lo_of(e[0]), bk_lo_of(e[1]), bk_lo_of(e[2]), bk_lo_of(e[3])};
+                const u16x4 hi = {bk_hi_of(e[0]), bk_hi_of(e[1]), bk_hi_of(e[2]), bk_hi_of(e[3])};
+                *reinterpret_cast<u4*>(bk_lo + s_base[s] + off) = lo;     // 16-B aligned (bases: 16-entry multiples)
+                *reinterpret_cast<u16x4*>(bk_hi + s_base[s] + off) = hi;  // 8-B aligned
             } else {  // the bucket is full (its estimate was low): the overflow list (folded at the end)
-                const u32 o = atomicAdd(&m->ovf_cur, e.y != ~0ull ? 2u : 1u);
-                if (o < ovf_cap) ovf[o] = e.x;
-                if (e.y != ~0ull && o + 1 < ovf_cap) ovf[o + 1] = e.y;
-                if (o + (e.y != ~0ull ? 1u : 0u) >= ovf_cap) m->spill = 1u;  // -> bucket_rest: the whole batch again
+                const u32 k = 1u + (e[1] != ~0ull) + (e[2] != ~0ull) + (e[3] != ~0ull);  // padding only at the end
+                const u32 o = atomicAdd(&m->ovf_cur, k);
+                for (u32 i = 0; i < k; ++i)
+                    if (o + i < ovf_cap) ovf[o + i] = e[i];
+                if (o + k > ovf_cap) m->spill = 1u;  // -> bucket_rest: the whole batch again
             }
         }
         __syncthreads();
     }
-    // the unused tails of this block's chunks: UNSEEN edges (P2 skips them)
+    // the unused tails of this block's chunks: padding entries (P2 skips them)
     for (u32 s = 0; s < ns; ++s)
-        for (u32 i = s_cpos[s] + threadIdx.x; i < s_cend[s]; i += P1B) bk[s_base[s] + i] = ~0ull;
+        for (u32 i = s_cpos[s] + threadIdx.x; i < s_cend[s]; i += P1B) bk_hi[s_base[s] + i] = kPadHi;
 }
 
 // Work items of P2 / P3: item i -> (slice i / cps, part i % cps) of a list of `len` entries; the part's range.
@@ -382,7 +419,8 @@ __device__ __forceinline__ void hook_g(u32* parent, u32 g, u32 v) {
 // them; `bk` = the slow array), C is then C | N, and its own slow edges go to `slow` (the bucket storage, free
 // by then). FINAL without SEG records those runs into `segs` (one per item with slow edges; null: none).
 template <bool FINAL, bool SEG = false>
-__global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict__ parent, const u64* __restrict__ bk,
+__global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict__ parent, const u32* __restrict__ bk_lo,
+                                                                const u16* __restrict__ bk_hi, const u64* __restrict__ bk,
                                                                 const u32* __restrict__ bits, u32 nwords32, u32 ns,
                                                                 Meta* __restrict__ m, u32* __restrict__ vl, u32 cps,
                                                                 u32 frac, u32 work_slot, u32 drain_at, u32 hub_only,
@@ -452,6 +490,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         u32 sl;
         u64 len, lo, hi;
         const u64* src = bk;
+        u64 ebase = 0;
         if constexpr (SEG) {
             const SlowSeg sg = segs[item];
             sl = sg.sl;
@@ -464,7 +503,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             len = m->bk_cur[sl] < m->bk_cap[sl] ? m->bk_cur[sl] : m->bk_cap[sl];
             if (!FINAL) len = len * frac >> 16;
             item_range(len, hub ? item : item % cps, cps, lo, hi);
-            src = bk + m->bk_base[sl];
+            ebase = m->bk_base[sl];
         }
         if (lo >= hi) continue;
         if (threadIdx.x == 0) seg_sl = sl;
@@ -473,35 +512,61 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             cur_slice = sl;
             __syncthreads();
         }
-        const u4* eb = reinterpret_cast<const u4*>(src);  // 16-B aligned (16-edge capacities; runs padded to pairs)
         const u32 sbase = sl << kSliceBits;
-        // pairs [lo / 2, ceil(hi / 2)); edges outside [lo, hi) are masked (a part may start or end mid-pair)
-        const u64 plo = lo / 2;
-        const u4* ep = eb + plo;  // this part's pairs, local (32-bit) indices from here on
-        const u32 np = (u32)((hi + 1) / 2 - plo);
-        const bool skip_first = lo & 1, skip_last = hi & 1;  // the part starts / ends in the middle of a pair
-        u4 q[kQ];
+        // SEG: u64 pairs [lo / 2, ceil(hi / 2)) of the slow list; buckets: 4-entry groups [lo / 4, ceil(hi / 4)) of the
+        // 6-B entries. Either way entries outside [lo, hi) are masked (a part may start or end mid-pair / mid-group).
+        const u64 plo = SEG ? lo / 2 : lo / 4;
+        const u32 np = SEG ? (u32)((hi + 1) / 2 - plo) : (u32)((hi + 3) / 4 - plo);
+        const u4* ep = reinterpret_cast<const u4*>(src) + plo;                        // SEG: pairs (16-B aligned)
+        const u4* elo = reinterpret_cast<const u4*>(bk_lo + ebase) + plo;             // buckets: 16-B aligned
+        const u64* ehi = reinterpret_cast<const u64*>(bk_hi + ebase) + plo;           // 8-B aligned
+        constexpr u32 kRoundItems = SEG ? kP2Round / 2 : kP2Round / 4;  // pairs or groups per round
+        constexpr int kL = SEG ? kQ : kP2Per / 4;                        // loads (of each stream) per thread
+        u4 q[kL];
+        u64 qh[kL];
         auto load_round = [&](u32 p0) {
 #pragma unroll
-            for (int k = 0; k < kQ; ++k) {
+            for (int k = 0; k < kL; ++k) {
                 const u32 j = p0 + (u32)k * kP2Block + threadIdx.x;
-                q[k] = __builtin_nontemporal_load(ep + (j < np ? j : np - 1));  // clamped: countable loads
+                const u32 jc = j < np ? j : np - 1;  // clamped: countable loads
+                if constexpr (SEG) {
+                    q[k] = __builtin_nontemporal_load(ep + jc);
+                } else {
+                    q[k] = __builtin_nontemporal_load(elo + jc);
+                    qh[k] = __builtin_nontemporal_load(ehi + jc);
+                }
             }
         };
         load_round(0);
-        for (u32 p0 = 0; p0 < np; p0 += kP2Round / 2) {
+        for (u32 p0 = 0; p0 < np; p0 += kRoundItems) {
             u32* s_cnt = s_cnt2 + rb * kMaxSlicesLds;
             u32 ua[kP2Per], va[kP2Per], rk[kP2Per];
             bool in[kP2Per];
+            if constexpr (SEG) {
+                const bool skip_first = lo & 1, skip_last = hi & 1;  // the part starts / ends in the middle of a pair
 #pragma unroll
-            for (int k = 0; k < kQ; ++k) {
-                const u32 j = p0 + (u32)k * kP2Block + threadIdx.x;
-                ua[2 * k] = q[k].x;
-                va[2 * k] = q[k].y;
-                ua[2 * k + 1] = q[k].z;
-                va[2 * k + 1] = q[k].w;
-                in[2 * k] = j < np && !(skip_first && j == 0) && ua[2 * k] != 0xFFFFFFFFu;  // UNSEEN: a chunk tail
-                in[2 * k + 1] = j < np && !(skip_last && j == np - 1) && ua[2 * k + 1] != 0xFFFFFFFFu;
+                for (int k = 0; k < kQ; ++k) {
+                    const u32 j = p0 + (u32)k * kP2Block + threadIdx.x;
+                    ua[2 * k] = q[k].x;
+                    va[2 * k] = q[k].y;
+                    ua[2 * k + 1] = q[k].z;
+                    va[2 * k + 1] = q[k].w;
+                    in[2 * k] = j < np && !(skip_first && j == 0) && ua[2 * k] != 0xFFFFFFFFu;  // UNSEEN: a pad
+                    in[2 * k + 1] = j < np && !(skip_last && j == np - 1) && ua[2 * k + 1] != 0xFFFFFFFFu;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < kL; ++k) {
+                    const u32 j = p0 + (u32)k * kP2Block + threadIdx.x;
+                    const u64 e0 = 4 * (plo + j);  // the group's first entry index in the bucket
+                    const u32 lv[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const u16 h16 = (u16)(qh[k] >> (16 * c));
+                        const bool real = bk_decode(lv[c], h16, sbase, ua[4 * k + c], va[4 * k + c]);
+                        in[4 * k + c] = j < np && real && e0 + c >= lo && e0 + c < hi;
+                    }
+                }
             }
             u32 bad = 0;
 #pragma unroll
@@ -510,7 +575,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 in[k] = in[k] && va[k] < cap;
             }
             if (bad) flag_err(err, kErrP2);
-            if (p0 + kP2Round / 2 < np) load_round(p0 + kP2Round / 2);  // next round in flight
+            if (p0 + kRoundItems < np) load_round(p0 + kRoundItems);  // next round in flight
             bool emit[kP2Per];
             u32 slow_m = 0;  // FINAL: this lane's slow edges (source not in C), bit k
 #pragma unroll

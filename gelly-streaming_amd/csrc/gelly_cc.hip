@@ -645,12 +645,16 @@ using gcc::inc_label;  // uf_device.h: shared with the host replay
 // read-only, no root moves during a compress, and a lane that reads a slot before or after its owner rewrites it
 // gets an ancestor either way (the old parent or the root). The pass then reads parent[] and writes only the
 // changed slots instead of streaming a second 4 B per id into the spare buffer.
-template <bool INPLACE>
+// CHECK (diagnostics, tune key inc_check): after the LDS fill every block also reads each bloom word with a
+// memory-side atomic (fresh by construction) and counts the words whose LDS copy differs: dbg[0] = words where the
+// memory holds a mark the LDS copy lacks (a lost mark: a wrong label can follow), dbg[1] = the reverse.
+template <bool INPLACE, bool CHECK>
 __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* parent, u32* labels,
                                                                  u32 n, const u32* __restrict__ bloom,
                                                                  u32* __restrict__ bloom_clear,
                                                                  const u32* __restrict__ giant_prev,
-                                                                 u32* __restrict__ giant_next, u64* __restrict__ bits) {
+                                                                 u32* __restrict__ giant_next, u64* __restrict__ bits,
+                                                                 u32* __restrict__ dbg) {
     trace_start(kTrCompressInc);
     extern __shared__ __attribute__((aligned(16))) u32 s_bloom[];
     __shared__ u32 s_g;
@@ -685,6 +689,23 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
         if (blockIdx.x == 0) *giant_next = s_g;
     }
     __syncthreads();
+    if constexpr (CHECK) {
+        for (u32 w = threadIdx.x; w < gcc::kBloomBits / 32; w += kIncBlock) {
+            const u32 mem = __hip_atomic_fetch_or(const_cast<u32*>(bloom) + w, 0u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            const u32 lds = s_bloom[w];
+            if (mem & ~lds) {
+                const u32 k = atomicAdd(&dbg[0], 1u);
+                if (k < 4) {
+                    dbg[16 + 4 * k] = blockIdx.x;
+                    dbg[17 + 4 * k] = w;
+                    dbg[18 + 4 * k] = lds;
+                    dbg[19 + 4 * k] = mem;
+                }
+            }
+            if (lds & ~mem) atomicAdd(&dbg[1], 1u);
+        }
+    }
     const u32 g = s_g;
     // kIncU chunks per wave in flight (one 16-B load each) before any is labelled: a wave that waited for each
     // chunk in turn kept ~4 MB in flight device-wide and streamed C5's 64 MB parent[] at ~2.2 TB/s
@@ -727,6 +748,41 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
                 if (!INPLACE || lab[k] != pk) labels[v0 + k] = lab[k];
             }
         chunk_bits(bits, nwords, nfull, lane, g, lab);
+    }
+}
+
+// Diagnostics (tune key inc_check): the incremental compress's labels vs the roots of the forest it started from
+// (`pre`, a copy taken just before it; quiescent here, so a plain walk is exact). dbg[2] counts wrong labels and
+// keeps the first four as (v, pre[v], label, root, is pre[v] marked in the bloom (memory-side reads), pre[pre[v]]);
+// dbg[3] = the bloom's set bits (its fill).
+__global__ __launch_bounds__(kBlock) void inc_verify_kernel(const u32* __restrict__ pre, const u32* __restrict__ labels,
+                                                            u32 n, const u32* __restrict__ bloom, u32* __restrict__ dbg) {
+    const u32 stride = gridDim.x * kBlock;
+    for (u32 w = blockIdx.x * kBlock + threadIdx.x; w < gcc::kBloomBits / 32; w += stride)
+        atomicAdd(&dbg[3], (u32)__builtin_popcount(bloom[w]));
+    for (u32 v = blockIdx.x * kBlock + threadIdx.x; v < n; v += stride) {
+        const u32 p = pre[v];
+        u32 r = p;
+        if (p != UNSEEN) {
+            r = v;
+            while (pre[r] < r) r = pre[r];
+        }
+        const u32 got = labels[v];
+        if (got == r) continue;
+        const u32 k = atomicAdd(&dbg[2], 1u);
+        if (k < 4) {
+            const u32 msk = gcc::bloom_mask(p);
+            const u32 word = __hip_atomic_fetch_or(const_cast<u32*>(bloom) + gcc::bloom_word(p), 0u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+            const u32 marked = (word & msk) == msk;
+            u32* o = dbg + 32 + 6 * k;
+            o[0] = v;
+            o[1] = p;
+            o[2] = got;
+            o[3] = r;
+            o[4] = marked;
+            o[5] = p < n ? pre[p] : UNSEEN;
+        }
     }
 }
 
@@ -1223,6 +1279,13 @@ __global__ void msg_header_kernel(u32* __restrict__ hdr, const u32* __restrict__
 //    own root), then the (v, label) lists.
 constexpr u32 kMaxPeers = 64;
 
+// The ids < n of bitmap word w: a peer's or a deserialized message's last word may carry bits past the id range
+// (a well-formed encode never sets them; gcc_forest_deserialize's bytes are untrusted), which must not index parent[].
+__device__ __forceinline__ u64 id_range_mask(u64 w, u32 n) {
+    const u64 lo = w * 64;
+    return lo + 64 <= n ? ~0ull : (lo >= n ? 0ull : (1ull << (n - lo)) - 1);
+}
+
 __global__ __launch_bounds__(kBlock) void msg_overlap_kernel(const char* __restrict__ msgs, u64 stride, u32 count,
                                                              u32 skip, u32 n, const u64* __restrict__ mine,
                                                              u32* __restrict__ witness) {
@@ -1239,7 +1302,8 @@ __global__ __launch_bounds__(kBlock) void msg_overlap_kernel(const char* __restr
         if (__hip_atomic_load(&witness[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != UNSEEN) continue;
         const u64 w = (t - (u64)p * chunks) * 64 + lane;
         u64 both = 0;
-        if (w < nw) both = reinterpret_cast<const u64*>(msgs + p * stride + GCC_MSG_HEADER_BYTES)[w] & mine[w];
+        if (w < nw)
+            both = reinterpret_cast<const u64*>(msgs + p * stride + GCC_MSG_HEADER_BYTES)[w] & mine[w] & id_range_mask(w, n);
         const unsigned long long wb = __ballot(both != 0);
         if (wb && lane == (u32)__builtin_ctzll(wb)) witness[p] = (u32)(w * 64 + __builtin_ctzll(both));  // any one
     }
@@ -1295,7 +1359,7 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict
             for (u32 p = 0; p < count; ++p)
                 if (s_g[p] != UNSEEN && s_w[p] != UNSEEN)
                     m |= reinterpret_cast<const u64*>(msgs + p * stride + GCC_MSG_HEADER_BYTES)[w];
-            if (m) m &= ~mine[w];
+            if (m) m &= ~mine[w] & id_range_mask(w, n);
             if (m && seen_oth) so = seen_oth[w];
         }
         if (newbits) {  // deferred: the new ids above R only go into newbits, the compress right after labels them
@@ -1385,7 +1449,7 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
         for (u64 w = wave; w < nw; w += waves) {
             u64 lone = 0;
             if (lane < count && s_g[lane] != UNSEEN && s_w[lane] == UNSEEN)
-                lone = reinterpret_cast<const u64*>(msgs + lane * stride + GCC_MSG_HEADER_BYTES)[w];
+                lone = reinterpret_cast<const u64*>(msgs + lane * stride + GCC_MSG_HEADER_BYTES)[w] & id_range_mask(w, n);
             const u64 v = w * 64 + lane;
             unsigned long long lb = __ballot(lone != 0);
             bool in_lone = false;
@@ -1461,6 +1525,47 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const u32* __restrict__ p
     }
 }
 
+// The parity digest of a compressed forest (= its canonical labels), as tests/golden/stream_digests.json and
+// oracle.label_digest compute it: out[2] += sum_v splitmix64((label[v] << 32) | v) mod 2^64, over every id (UNSEEN
+// labels included); out[0] += #seen, out[1] += #roots. Lets a test check every window of a long stream without
+// copying 4 B per id to the host.
+__device__ __forceinline__ u64 splitmix_fin(u64 x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void digest_kernel(const u32* __restrict__ labels, u32 n,
+                                                        unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long s_acc[3][kBlock / 64];
+    const u64 stride = (u64)gridDim.x * kBlock;
+    unsigned long long seen = 0, roots = 0, dig = 0;
+    for (u64 v = (u64)blockIdx.x * kBlock + threadIdx.x; v < n; v += stride) {
+        const u32 l = labels[v];
+        seen += (l != UNSEEN);
+        roots += (l == v);
+        dig += splitmix_fin(((u64)l << 32) | v);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        seen += __shfl_down(seen, off, 64);
+        roots += __shfl_down(roots, off, 64);
+        dig += __shfl_down(dig, off, 64);
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        s_acc[0][wave] = seen;
+        s_acc[1][wave] = roots;
+        s_acc[2][wave] = dig;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        unsigned long long a = 0;
+        for (int w = 0; w < kBlock / 64; ++w) a += s_acc[threadIdx.x][w];
+        atomicAdd(&out[threadIdx.x], a);  // mod 2^64, like the digest
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void gen_kernel(gcc_gen_params prm, u64 first, u64 count, uint2* __restrict__ out) {
     const u64 stride = (u64)gridDim.x * kBlock;
     for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < count; i += stride) {
@@ -1518,6 +1623,9 @@ struct FoldTune {
     // to a ~60 % false-hit rate, so the incremental compress walks for most ids anyway; and in two full-suite runs
     // that window's incremental compress left ONE label stale (not root-caused). C5 (1/256) keeps it.
     u64 inc_div = 64;
+    // diagnostics: every incremental compress is checked against the roots of the forest it started from and its
+    // bloom LDS copies against memory-side reads; failures go to stderr and to gcc_forest_inc_check_stats
+    bool inc_check = false;
     // bucketed fold of a fresh forest (bucket_fold.h): batches of >= bucket_min_batch edges over >= bucket_min_ids
     // ids (default: exactly the forests whose giant bitmap does not fit LDS); seeding = bucket_levels P2 + P3 levels
     // over the first bucket_sample of every bucket
@@ -1571,6 +1679,9 @@ struct gcc_forest {
     int bloom_cur = 0;
     bool rec_all = false;
     u32* bloom(int i) const { return d_bloom + (size_t)i * (gcc::kBloomBits / 32); }
+    u32* d_dbg = nullptr;  // tune inc_check: 64 words (compress_inc_kernel<.., true>, inc_verify_kernel)
+    u32* h_dbg = nullptr;
+    u64 inc_checks = 0, inc_bad_labels = 0, inc_lost_marks = 0;
 
     // pinned double-buffered staging for host-fed edges (per-edge foldEdges appends here)
     static constexpr u64 kStageEdges = 1ull << 20;  // 8 MiB per slot
@@ -1606,8 +1717,8 @@ struct gcc_forest {
 
     // bucketed fold (bucket_fold.h): metadata, bucket storage, overflow list, v-lists (grown on demand)
     bk::Meta* d_meta = nullptr;
-    u64* d_bk = nullptr;
-    u64 bk_cap_edges = 0;
+    uint8_t* d_bk = nullptr;  // bucket storage: bk::bk_bytes(S) bytes = S 6-B entries (lo array, then hi array)
+    u64 bk_cap_bytes = 0;
     u64* d_ovf = nullptr;
     u64 ovf_cap = 0;
     u32* d_vl = nullptr;
@@ -1766,6 +1877,43 @@ static bool inc_forest(const gcc_forest* h) {
            ((reinterpret_cast<uintptr_t>(h->d_parent) | reinterpret_cast<uintptr_t>(h->d_spare)) & 15) == 0;
 }
 
+// tune inc_check (diagnostics): zero the debug words and, for the in-place compress, keep a copy of the forest it
+// starts from in d_spare (free: an in-place compress does not swap)
+static int inc_check_begin(gcc_forest* h, bool inplace) {
+    if (!h->d_dbg) {
+        HIP_TRY(hipMalloc((void**)&h->d_dbg, 64 * sizeof(u32)));
+        HIP_TRY(hipHostMalloc((void**)&h->h_dbg, 64 * sizeof(u32), hipHostMallocDefault));
+    }
+    HIP_TRY(hipMemsetAsync(h->d_dbg, 0, 64 * sizeof(u32), h->stream));
+    if (inplace) HIP_TRY(hipMemcpyAsync(h->d_spare, h->d_parent, (size_t)h->cap * sizeof(u32), hipMemcpyDeviceToDevice,
+                                        h->stream));
+    return GCC_OK;
+}
+
+static int inc_check_end(gcc_forest* h, const u32* pre, const u32* labels, const u32* bloom) {
+    hipLaunchKernelGGL(inc_verify_kernel, dim3(kMaxGrid), dim3(kBlock), 0, h->stream, pre, labels, h->cap, bloom, h->d_dbg);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(h->h_dbg, h->d_dbg, 64 * sizeof(u32), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    const u32* d = h->h_dbg;
+    ++h->inc_checks;
+    h->inc_lost_marks += d[0];
+    h->inc_bad_labels += d[2];
+    if (d[0] || d[2]) {
+        fprintf(stderr, "[inc_check] compress %llu: bloom fill %u bits; LDS words missing marks %u (extra %u); wrong labels %u\n",
+                (unsigned long long)h->inc_checks, d[3], d[0], d[1], d[2]);
+        for (u32 k = 0; k < std::min<u32>(d[0], 4); ++k)
+            fprintf(stderr, "[inc_check]   block %u word %u: lds %08x memory %08x\n", d[16 + 4 * k], d[17 + 4 * k],
+                    d[18 + 4 * k], d[19 + 4 * k]);
+        for (u32 k = 0; k < std::min<u32>(d[2], 4); ++k) {
+            const u32* o = d + 32 + 6 * k;
+            fprintf(stderr, "[inc_check]   v %u: pre parent %u (marked in memory %u, its parent %u) label %u root %u\n", o[0],
+                    o[1], o[4], o[5], o[2], o[3]);
+        }
+    }
+    return GCC_OK;
+}
+
 // compress into the spare buffer and swap; with the filter on, refresh the giant bitmap from the new labels.
 // Incremental (compress_inc_kernel) when every mutation since the last compress was recorded.
 // oth (the merge encode): a full compress also writes the others mask of every 64-id word (chunk_oth); returns
@@ -1796,14 +1944,32 @@ static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth =
         if (!rc && inc_here && h->rec_all) {
             const char* kname = std::strcmp(name, "refresh") ? "compress_inc" : "refresh_inc";
             inplace = h->tune.inc_inplace;
-            rc = inplace ? launch_k(h, kname, 0, compress_inc_kernel<true>, dim3(h->n_cu), dim3(kIncBlock),
-                                    gcc::kBloomBits / 8, (const u32*)h->d_parent, h->d_parent, h->cap,
-                                    (const u32*)h->bloom(h->bloom_cur), clear, (const u32*)(h->d_giant + h->giant_slot),
-                                    h->d_giant + (h->giant_slot ^ 1), h->d_bits)
-                         : launch_k(h, kname, 0, compress_inc_kernel<false>, dim3(h->n_cu), dim3(kIncBlock),
-                                    gcc::kBloomBits / 8, (const u32*)h->d_parent, h->d_spare, h->cap,
-                                    (const u32*)h->bloom(h->bloom_cur), clear, (const u32*)(h->d_giant + h->giant_slot),
-                                    h->d_giant + (h->giant_slot ^ 1), h->d_bits);
+            const bool check = h->tune.inc_check;
+            if (check) rc = inc_check_begin(h, inplace);
+            const u32* bl = h->bloom(h->bloom_cur);
+            const u32* gp = h->d_giant + h->giant_slot;
+            u32* gn = h->d_giant + (h->giant_slot ^ 1);
+            u32* out = inplace ? h->d_parent : h->d_spare;
+            if (!rc) {
+                if (inplace && check)
+                    rc = launch_k(h, kname, 0, compress_inc_kernel<true, true>, dim3(h->n_cu), dim3(kIncBlock),
+                                  gcc::kBloomBits / 8, (const u32*)h->d_parent, out, h->cap, bl, clear, gp, gn, h->d_bits,
+                                  h->d_dbg);
+                else if (inplace)
+                    rc = launch_k(h, kname, 0, compress_inc_kernel<true, false>, dim3(h->n_cu), dim3(kIncBlock),
+                                  gcc::kBloomBits / 8, (const u32*)h->d_parent, out, h->cap, bl, clear, gp, gn, h->d_bits,
+                                  (u32*)nullptr);
+                else if (check)
+                    rc = launch_k(h, kname, 0, compress_inc_kernel<false, true>, dim3(h->n_cu), dim3(kIncBlock),
+                                  gcc::kBloomBits / 8, (const u32*)h->d_parent, out, h->cap, bl, clear, gp, gn, h->d_bits,
+                                  h->d_dbg);
+                else
+                    rc = launch_k(h, kname, 0, compress_inc_kernel<false, false>, dim3(h->n_cu), dim3(kIncBlock),
+                                  gcc::kBloomBits / 8, (const u32*)h->d_parent, out, h->cap, bl, clear, gp, gn, h->d_bits,
+                                  (u32*)nullptr);
+            }
+            // the forest the compress started from: the copy in d_spare (in place), or d_parent itself
+            if (!rc && check) rc = inc_check_end(h, inplace ? h->d_spare : h->d_parent, out, bl);
         } else if (!rc) {
             rc = launch_k(h, name, 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)), dim3(kBlock), 0,
                           h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
@@ -2045,7 +2211,10 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     }
     const u32 p1_blocks = 2 * (u32)h->n_cu;  // (bucket_p1 = 1 runs n_cu blocks: fewer writers, same slack bound)
     const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
-    if ((rc = grow(h->d_bk, h->bk_cap_edges, bk::storage_edges(n, ns, p1_blocks), h->stream))) return rc;
+    const u64 bk_S = bk::bk_entries(bk::storage_edges(n, ns, p1_blocks));  // entries (a multiple of 16)
+    if ((rc = grow(h->d_bk, h->bk_cap_bytes, bk::bk_bytes(bk_S), h->stream))) return rc;
+    u32* bk_lo = reinterpret_cast<u32*>(h->d_bk);
+    bk::u16* bk_hi = reinterpret_cast<bk::u16*>(h->d_bk + 4 * bk_S);
     if ((rc = grow(h->d_ovf, h->ovf_cap, n / 8 + 65536, h->stream))) return rc;
     if ((rc = grow(h->d_vl, h->vl_cap, bk::storage_edges(n, ns, p2_blocks), h->stream))) return rc;
     // room for half the batch in the slow lists (C4: 3.9 % slow; C4's 1/8 share: more than the 12.5 % an n/8
@@ -2080,9 +2249,9 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (!rc)
         rc = t.bucket_p1 == 1
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16>, dim3(h->n_cu), dim3(1024), bk::p1_lds(1024, 16),
-                            edges, n, ns, h->cap, h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err)
+                            edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err)
                  : launch_k(h, "bucket", n, bk::bucket_kernel<512, 16>, dim3(p1_blocks), dim3(512), bk::p1_lds(512, 16),
-                            edges, n, ns, h->cap, h->d_meta, h->d_bk, h->d_ovf, ovf_cap, h->d_err);
+                            edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err);
     if (rc) return rc;
     // seeding: C := {hub}, then levels over the sample
     HIP_TRY(hipMemsetAsync(bits, 0, (size_t)nw32 * sizeof(u32), h->stream));
@@ -2094,8 +2263,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     for (int l = 0; l < levels && !rc; ++l) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
         rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
-                      f_lds, h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl,
-                      l == 0 ? cps_hub : cps_seed, l == 0 ? frac_hub : frac, slot++, h->tune.drain_at, (u32)(l == 0),
+                      f_lds, h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,
+                      (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, l == 0 ? cps_hub : cps_seed, l == 0 ? frac_hub : frac, slot++, h->tune.drain_at, (u32)(l == 0),
                       (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err,
                       (bk::SlowSeg*)nullptr);
         if (!rc)
@@ -2109,7 +2278,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
     rc = launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true>, dim3(p2_blocks), dim3(bk::kP2Block), f_lds,
-                  h->d_parent, (const u64*)h->d_bk, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, cps, 65536u, slot++,
+                  h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr, (const u32*)bits, nw32, ns,
+                  h->d_meta, h->d_vl, cps, 65536u, slot++,
                   h->tune.drain_at, 0u, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr);
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
@@ -2126,11 +2296,13 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u64* slow_list = h->d_slow;
     u32 slow_list_cap = slow_cap;
     if (slow2 && !rc) {
-        const u32 slow_cap2 = (u32)std::min<u64>(0x7FFFFFFEull, h->bk_cap_edges / p2_blocks) & ~1u;
+        // the bucket storage (consumed by FINAL P2) as u64 slow entries
+        const u32 slow_cap2 = (u32)std::min<u64>(0x7FFFFFFEull, h->bk_cap_bytes / 8 / p2_blocks) & ~1u;
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
         rc = launch_k(h, "slice_filter2", 0, bk::slice_filter_kernel<true, true>, dim3(p2_blocks), dim3(bk::kP2Block),
-                      f_lds, h->d_parent, (const u64*)h->d_slow, (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, 1u,
-                      65536u, slot++, h->tune.drain_at, 0u, (const u32*)giant, h->d_bk, slow_cap2, h->cap, h->d_err, h->d_seg);
+                      f_lds, h->d_parent, (const u32*)nullptr, (const bk::u16*)nullptr, (const u64*)h->d_slow,
+                      (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, 1u, 65536u, slot++, h->tune.drain_at, 0u,
+                      (const u32*)giant, reinterpret_cast<u64*>(h->d_bk), slow_cap2, h->cap, h->d_err, h->d_seg);
         if (!rc)
             rc = launch_k(h, "slice_hook2", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
                           h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
@@ -2140,7 +2312,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                                   (const bk::Meta*)h->d_meta)
                        : launch_k(h, "bucket_hook2", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock),
                                   0, h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
-        slow_list = h->d_bk;
+        slow_list = reinterpret_cast<const u64*>(h->d_bk);
         slow_list_cap = slow_cap2;
     }
     if (!rc)
@@ -2348,7 +2520,7 @@ static int refresh_host(gcc_forest* h) {
 static int counts(gcc_forest* h, unsigned long long out[2]) {
     int rc = flush(h);
     if (rc) return rc;
-    if (!h->d_counts) HIP_TRY(hipMalloc((void**)&h->d_counts, 2 * sizeof(unsigned long long)));
+    if (!h->d_counts) HIP_TRY(hipMalloc((void**)&h->d_counts, 3 * sizeof(unsigned long long)));
     HIP_TRY(hipMemsetAsync(h->d_counts, 0, 2 * sizeof(unsigned long long), h->stream));
     hipLaunchKernelGGL(count_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent, h->cap,
                        h->d_counts);
@@ -2360,6 +2532,26 @@ static int counts(gcc_forest* h, unsigned long long out[2]) {
 // C ABI
 // ------------------------------------------------------------------------------------------------
 extern "C" {
+
+int gcc_forest_label_digest(gcc_forest* h, uint64_t* digest, uint64_t* n_seen, uint64_t* n_components) {
+    CHECK_ARG(h && digest, "null argument");
+    DeviceGuard g(h->device);
+    int rc = compress_async(h);
+    if (rc) return rc;
+    if (!h->d_counts) HIP_TRY(hipMalloc((void**)&h->d_counts, 3 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(h->d_counts, 0, 3 * sizeof(unsigned long long), h->stream));
+    hipLaunchKernelGGL(digest_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent, h->cap,
+                       h->d_counts);
+    HIP_TRY(hipGetLastError());
+    unsigned long long c[3];
+    HIP_TRY(hipMemcpyAsync(c, h->d_counts, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+    rc = stream_sync_checked(h);
+    if (rc) return rc;
+    *digest = c[2];
+    if (n_seen) *n_seen = c[0];
+    if (n_components) *n_components = c[1];
+    return GCC_OK;
+}
 
 const char* gcc_last_error(void) { return g_last_error.c_str(); }
 
@@ -2457,8 +2649,10 @@ static int set_lds_attrs_impl() {
         const void* f;
         int bytes;
     } tab[] = {
-        {(const void*)compress_inc_kernel<false>, (int)(gcc::kBloomBits / 8)},
-        {(const void*)compress_inc_kernel<true>, (int)(gcc::kBloomBits / 8)},
+        {(const void*)compress_inc_kernel<false, false>, (int)(gcc::kBloomBits / 8)},
+        {(const void*)compress_inc_kernel<true, false>, (int)(gcc::kBloomBits / 8)},
+        {(const void*)compress_inc_kernel<false, true>, (int)(gcc::kBloomBits / 8)},
+        {(const void*)compress_inc_kernel<true, true>, (int)(gcc::kBloomBits / 8)},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, false>, filtered},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true, false>, filtered},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, true>, filtered},
@@ -2566,6 +2760,8 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (h->d_msg_oth) (void)hipFree(h->d_msg_oth);
     if (h->d_bits) (void)hipFree(h->d_bits);
     if (h->d_bloom) (void)hipFree(h->d_bloom);
+    if (h->d_dbg) (void)hipFree(h->d_dbg);
+    if (h->h_dbg) (void)hipHostFree(h->h_dbg);
     if (h->d_giant) (void)hipFree(h->d_giant);
     if (h->d_flags) (void)hipFree(h->d_flags);
     if (h->d_bmin) (void)hipFree(h->d_bmin);
@@ -3102,11 +3298,13 @@ int gcc_forest_deserialize(gcc_forest* h, const void* in, uint64_t size) {
     std::memcpy(&hd, in, sizeof(hd));
     CHECK_ARG(hd.magic == GCC_SER_MAGIC && hd.version == 1, "not a serialized gelly summary (magic / version)");
     CHECK_ARG(hd.id_capacity <= h->cap, "serialized summary has a larger id range than the forest");
-    CHECK_ARG(size >= GCC_SER_HEADER_BYTES + hd.payload, "serialized summary truncated");
+    // compared without arithmetic on the untrusted fields (a wrapped n_seen or payload must not pass)
+    CHECK_ARG(hd.payload <= size - GCC_SER_HEADER_BYTES, "serialized summary truncated");
     DeviceGuard g(h->device);
     const u8* body = static_cast<const u8*>(in) + GCC_SER_HEADER_BYTES;
     if (hd.kind == 1) {
-        CHECK_ARG(hd.payload == 8 * hd.n_seen, "serialized pairs: bad length");
+        CHECK_ARG(hd.payload % 8 == 0 && hd.n_seen == hd.payload / 8 && hd.n_seen <= (u64)hd.id_capacity,
+                  "serialized pairs: bad length");
         return gcc_forest_fold_host(h, reinterpret_cast<const u32*>(body), hd.n_seen);  // ids validated there
     }
     CHECK_ARG(hd.kind == 2, "serialized summary: unknown kind");
@@ -3230,6 +3428,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "refresh_labels") t.refresh_labels = value != 0;
     else if (k == "inc_min_ids") t.inc_min_ids = (u64)value;
     else if (k == "inc_div") t.inc_div = std::max<u64>(1, (u64)value);
+    else if (k == "inc_check") t.inc_check = value != 0;
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = (int)value == 1 ? 1 : 0;
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
@@ -3302,6 +3501,14 @@ int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size) {
     h->slow_rounds.clear();
     if (out.size() + 1 > size) return set_err(GCC_E_INVALID, "profile buffer too small (%zu bytes needed)", out.size() + 1);
     snprintf(buf, size, "%s", out.c_str());
+    return GCC_OK;
+}
+
+int gcc_forest_inc_check_stats(gcc_forest* h, uint64_t* checks, uint64_t* bad_labels, uint64_t* lost_marks) {
+    CHECK_ARG(h && checks && bad_labels && lost_marks, "null argument");
+    *checks = h->inc_checks;
+    *bad_labels = h->inc_bad_labels;
+    *lost_marks = h->inc_lost_marks;
     return GCC_OK;
 }
 

@@ -38,6 +38,7 @@ struct Rccl {
     ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
     ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
@@ -64,6 +65,7 @@ Rccl& rccl() {
         r.CommInitRank = (decltype(r.CommInitRank))sym("ncclCommInitRank");
         r.CommInitAll = (decltype(r.CommInitAll))sym("ncclCommInitAll");
         r.CommDestroy = (decltype(r.CommDestroy))sym("ncclCommDestroy");
+        r.CommAbort = (decltype(r.CommAbort))sym("ncclCommAbort");
         r.AllGather = (decltype(r.AllGather))sym("ncclAllGather");
         r.GroupStart = (decltype(r.GroupStart))sym("ncclGroupStart");
         r.GroupEnd = (decltype(r.GroupEnd))sym("ncclGroupEnd");
@@ -108,6 +110,10 @@ struct gcc_comm {
     bool prefer_labels = false;
     u64 last_bytes = 0;    // bytes each rank contributed to the last merge's all_gather
     int last_rounds = 0;
+    // a merge failed where the ranks could not agree on it (e.g. a buffer allocation before the collective): the
+    // communicator was aborted and is unusable; the peers may be left inside the collective, so the job's ranks must
+    // all be torn down (as a failed Flink task restarts the job)
+    bool broken = false;
 };
 
 namespace {
@@ -131,12 +137,23 @@ int forest_info(gcc_forest* h, int* dev, u32* V, hipStream_t* s) {
     return GCC_OK;
 }
 
+// A failure no peer can learn of in-band: abort the communicator (gcc_comm.broken) and return the error.
+int fail_comm(gcc_comm* c, int rc) {
+    c->broken = true;
+    if (c->comm && rccl().CommAbort) (void)rccl().CommAbort(c->comm);
+    c->comm = nullptr;
+    return rc;
+}
+
 // The label-array exchange (no dominant component): all_gather of the canonical labels, absorb the others.
 int merge_labels_rccl(gcc_forest* h, gcc_comm* c, u32 V, hipStream_t st) {
     const u32* lab = nullptr;
-    ABI_TRY(gcc_forest_labels_device(h, &lab));
-    ABI_TRY(ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * V * sizeof(u32)));
-    NCCL_TRY(rccl().AllGather(lab, c->d_recv, V, ncclUint32, c->comm, st));
+    int rc = gcc_forest_labels_device(h, &lab);
+    if (!rc) rc = ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * V * sizeof(u32));
+    if (rc) return fail_comm(c, rc);  // before the collective: the peers cannot learn of it
+    const ncclResult_t r = rccl().AllGather(lab, c->d_recv, V, ncclUint32, c->comm, st);
+    if (r != ncclSuccess)
+        return fail_comm(c, gcc_set_err(GCC_E_HIP, "ncclAllGather (labels): %s", rccl().GetErrorString(r)));
     for (int p = 0; p < c->nranks; ++p)
         if (p != c->rank)
             ABI_TRY(gcc_forest_merge_labels_device(h, static_cast<const u32*>(c->d_recv) + (u64)p * V, V));
@@ -220,6 +237,7 @@ int gcc_comm_info(gcc_comm* c, int* nranks, int* rank, uint64_t* last_bytes) {
 // the union of all of them, compressed. Synchronises the forest's stream (it reads the gathered headers).
 int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
     CHECK_ARG(h && c, "null argument");
+    CHECK_ARG(!c->broken, "communicator aborted by an earlier failed merge: destroy it (its peers' too)");
     int dev;
     u32 V;
     hipStream_t st;
@@ -230,6 +248,10 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
     if (!c->h_hdr) HIP_TRY(hipHostMalloc((void**)&c->h_hdr, (size_t)c->nranks * 16, hipHostMallocDefault));
     if (c->cap_others == 0) c->cap_others = std::max<u64>(1024, V / 64);
     c->last_rounds = 0;
+    // Every rank takes the same decisions (sizes, repeats) from the gathered headers. A rank whose own encode or
+    // absorb fails keeps following them and sends a failed-status header (include/gelly_cc.h) in the next round,
+    // so every rank leaves the loop together with an error instead of one rank leaving its peers in a collective.
+    int local_rc = GCC_OK;
     while (!c->prefer_labels) {
         const u64 cap = c->cap_others;
         const u64 size = round16(gcc_msg_bytes(V, cap));
@@ -237,25 +259,44 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
             c->prefer_labels = true;
             break;
         }
-        ABI_TRY(ensure(c->d_send, c->send_bytes, size));
-        ABI_TRY(ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * size));
-        ABI_TRY(gcc_forest_encode(h, c->d_send, cap));
-        NCCL_TRY(rccl().AllGather(c->d_send, c->d_recv, (size_t)size, ncclUint8, c->comm, st));
-        ABI_TRY(gcc_forest_absorb_many(h, c->d_recv, size, (u32)c->nranks, (u32)c->rank, cap));
-        HIP_TRY(hipMemcpy2DAsync(c->h_hdr, 16, c->d_recv, (size_t)size, 16, (size_t)c->nranks, hipMemcpyDeviceToHost, st));
-        ABI_TRY(gcc_forest_compress(h));
-        HIP_TRY(hipStreamSynchronize(st));
+        int rc = ensure(c->d_send, c->send_bytes, size);
+        if (!rc) rc = ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * size);
+        if (rc) return fail_comm(c, rc);
+        if (!local_rc) local_rc = gcc_forest_encode(h, c->d_send, cap);
+        if (local_rc) {  // a header the absorb skips (id_capacity 0) and every rank reads as "the merge failed"
+            const u32 hdr[4] = {0xFFFFFFFFu, 0, 0, GCC_MSG_STATUS_FAILED};
+            rc = hipMemcpyAsync(c->d_send, hdr, sizeof(hdr), hipMemcpyHostToDevice, st) == hipSuccess ? GCC_OK
+                 : gcc_set_err(GCC_E_HIP, "failed-status header copy");
+            if (!rc) rc = hipStreamSynchronize(st) == hipSuccess ? GCC_OK : gcc_set_err(GCC_E_HIP, "stream sync");
+            if (rc) return fail_comm(c, rc);
+        }
+        const ncclResult_t r = rccl().AllGather(c->d_send, c->d_recv, (size_t)size, ncclUint8, c->comm, st);
+        if (r != ncclSuccess)
+            return fail_comm(c, gcc_set_err(GCC_E_HIP, "ncclAllGather (messages): %s", rccl().GetErrorString(r)));
+        if (!local_rc) local_rc = gcc_forest_absorb_many(h, c->d_recv, size, (u32)c->nranks, (u32)c->rank, cap);
+        if (hipMemcpy2DAsync(c->h_hdr, 16, c->d_recv, (size_t)size, 16, (size_t)c->nranks, hipMemcpyDeviceToHost, st) !=
+                hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return fail_comm(c, gcc_set_err(GCC_E_HIP, "gathered headers: %s", hipGetErrorString(hipGetLastError())));
+        if (!local_rc) local_rc = gcc_forest_compress(h);
         ++c->last_rounds;
         c->last_bytes = size;
         u64 nmax = 0;
-        for (int p = 0; p < c->nranks; ++p) nmax = std::max<u64>(nmax, c->h_hdr[4 * p + 1]);
+        int failed = -1;
+        for (int p = 0; p < c->nranks; ++p) {
+            nmax = std::max<u64>(nmax, c->h_hdr[4 * p + 1]);
+            if (c->h_hdr[4 * p + 3] == GCC_MSG_STATUS_FAILED && failed < 0) failed = p;
+        }
+        if (failed >= 0)
+            return local_rc ? local_rc : gcc_set_err(GCC_E_INTERNAL, "group merge: rank %d failed (its error is on that rank)", failed);
         if (nmax <= cap) {
             if (4 * nmax < cap && cap > 1024) c->cap_others = std::max<u64>({1024, 3 * nmax / 2, cap / 2});
-            return GCC_OK;
+            return local_rc;  // the peers finish too: an error here is this rank's own
         }
         c->cap_others = std::max<u64>(3 * nmax / 2, 2 * cap);  // some list did not fit: again, larger
     }
     ++c->last_rounds;
+    if (local_rc) return fail_comm(c, local_rc);
     return merge_labels_rccl(h, c, V, st);
 }
 

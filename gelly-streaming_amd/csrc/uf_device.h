@@ -129,31 +129,31 @@ struct Count {
 // p that is some id's parent is still a root: that id's label is p, no find needed. Ids that leave UNSEEN need
 // no mark: one hung straight under a root never becomes a parent value, one made a root is marked if hooked.
 constexpr u32 kBloomBits = 1u << 20;  // 128 KiB: one CU's LDS copy in the incremental compress
-// kBloomK bits per mark (independent multiplicative hashes): at C5's 65K marks per window in 1M bits the false-hit
-// rate is 6.0 % with one bit, 1.5 % with two; every false hit costs the compress one random read of parent[p]
-constexpr int kBloomK = 2;
-UF_HD u32 bloom_slot(u32 x, int i) { return (x * (i == 0 ? 0x9E3779B1u : 0x85EBCA77u)) >> 12; }
-UF_HD bool bloom_test(const u32* bloom, u32 x) {
-    bool hit = true;
+// A BLOCKED bloom filter (round 3): a mark sets kBloomK bits of ONE 32-bit word (the word and the bits from two
+// independent hashes), so marking is one memory-side atomicOr and a test one LDS read. Round 2's filter set 2 bits
+// in 2 words: two atomics per hook in the fold (the fold of a short window is bound by memory-side atomics) and a
+// 1.4 % false-hit rate at C5's 65K marks per window; 4 bits in one of 32K words: ~0.8 %.
+constexpr int kBloomK = 4;
+UF_HD u32 bloom_word(u32 x) { return (x * 0x9E3779B1u) >> 17; }  // 15 bits: one of kBloomBits / 32 words
+UF_HD u32 bloom_mask(u32 x) {
+    u32 h = x * 0x85EBCA77u;
+    h ^= h >> 15;
+    h *= 0xC2B2AE3Du;
+    u32 m = 0;
     UF_UNROLL
-    for (int i = 0; i < kBloomK; ++i) {
-        const u32 s = bloom_slot(x, i);
-        hit = hit && ((bloom[s >> 5] >> (s & 31)) & 1u);
-    }
-    return hit;
+    for (int i = 0; i < kBloomK; ++i) m |= 1u << ((h >> (27 - 5 * i)) & 31);
+    return m;
+}
+UF_HD bool bloom_test(const u32* bloom, u32 x) {
+    const u32 m = bloom_mask(x);
+    return (bloom[bloom_word(x)] & m) == m;
 }
 struct NoRec {
     UF_HD void mark(u32) const {}
 };
 struct BloomRec {
     u32* bloom;
-    UF_HD void mark(u32 x) const {
-        UF_UNROLL
-        for (int i = 0; i < kBloomK; ++i) {
-            const u32 s = bloom_slot(x, i);
-            aor(&bloom[s >> 5], 1u << (s & 31));
-        }
-    }
+    UF_HD void mark(u32 x) const { aor(&bloom[bloom_word(x)], bloom_mask(x)); }
 };
 
 template <class L, bool SPLIT, class C = NoCount>

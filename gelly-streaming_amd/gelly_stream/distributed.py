@@ -124,6 +124,8 @@ class RcclComm:
         from .native import call
 
         call("gcc_forest_group_merge", ds.handle, self._h)
+        if hasattr(ds, "_dirty"):  # the forest changed under the Python view: drop its cached labels
+            ds._dirty()
 
     def last_bytes(self) -> int:
         from .native import call

@@ -307,6 +307,19 @@ class DisjointSet:
         for k, v in knobs.items():
             call("gcc_forest_tune", self.handle, k.encode(), float(v))
 
+    def label_digest(self) -> tuple:
+        """(digest, seen, components) of the canonical labels, computed on the device (gcc_forest_label_digest): the
+        digest of tests/golden/stream_digests.json / oracle.label_digest, without a host copy of the labels."""
+        a, b, c = c_uint64(), c_uint64(), c_uint64()
+        call("gcc_forest_label_digest", self.handle, byref(a), byref(b), byref(c))
+        return a.value, b.value, c.value
+
+    def inc_check_stats(self) -> tuple:
+        """Diagnostics (tune(inc_check=1)): (checked incremental compresses, wrong labels, lost bloom marks)."""
+        a, b, c = c_uint64(), c_uint64(), c_uint64()
+        call("gcc_forest_inc_check_stats", self.handle, byref(a), byref(b), byref(c))
+        return a.value, b.value, c.value
+
     def copy(self) -> "DisjointSet":
         """A fresh forest with the same partition (Flink copies the fold's initial value per window)."""
         d = DisjointSet(self.id_capacity, self.device)

@@ -84,3 +84,73 @@ FN(void, deserialize)(JNIEnv* env, jclass c, jlong h, jbyteArray data) {
     (*env)->ReleaseByteArrayElements(env, data, p, JNI_ABORT);
     fail(env, rc);
 }
+
+/* ---- Long vertex ids (DisjointSet<Long> takes any Long, …/summaries/DisjointSet.java:30-34): the id dictionary of
+ * include/gelly_cc.h, gcc_idmap_* ---- */
+#define M(x) ((gcc_idmap*)(intptr_t)(x))
+
+FN(jlong, idmapCreate)(JNIEnv* env, jclass c, jint capacity) {
+    gcc_idmap* m = 0;
+    if (fail(env, gcc_idmap_create((uint32_t)capacity, &m))) return 0;
+    return (jlong)(intptr_t)m;
+}
+
+FN(void, idmapDestroy)(JNIEnv* env, jclass c, jlong m) { (void)gcc_idmap_destroy(M(m)); }
+
+/* nPairs (Long src, Long dst) pairs: map every id to its dense id straight into the pinned staging slot, then
+ * submit the slot (the same call sequence as a direct-id batch: staging -> fill -> submit) */
+FN(void, submitLong)(JNIEnv* env, jclass c, jlong h, jlong m, jlongArray pairs, jint nPairs) {
+    uint32_t* slot = 0;
+    uint64_t cap = 0;
+    if (fail(env, gcc_forest_staging(H(h), &slot, &cap))) return;
+    if ((uint64_t)nPairs > cap) {
+        fail(env, GCC_E_INVALID);
+        return;
+    }
+    jlong* p = (*env)->GetLongArrayElements(env, pairs, 0);
+    int rc = gcc_idmap_map(M(m), (const int64_t*)p, 2 * (uint64_t)nPairs, slot);
+    (*env)->ReleaseLongArrayElements(env, pairs, p, JNI_ABORT);
+    if (fail(env, rc)) return;
+    fail(env, gcc_forest_submit(H(h), (uint64_t)nPairs));
+}
+
+/* dense id of `id`, or -1 (GCC_UNSEEN) if it was never mapped */
+FN(jint, idmapLookup)(JNIEnv* env, jclass c, jlong m, jlong id) {
+    uint32_t d = GCC_UNSEEN;
+    if (fail(env, gcc_idmap_lookup(M(m), (int64_t)id, &d))) return -1;
+    return (jint)d;
+}
+
+/* out[d] = original id of dense id d, for every mapped id */
+FN(jlongArray, idmapIds)(JNIEnv* env, jclass c, jlong m) {
+    uint64_t n = 0;
+    if (fail(env, gcc_idmap_size(M(m), &n))) return 0;
+    jlongArray out = (*env)->NewLongArray(env, (jsize)n);
+    jlong* p = (*env)->GetLongArrayElements(env, out, 0);
+    const int rc = gcc_idmap_ids(M(m), (int64_t*)p, n);
+    (*env)->ReleaseLongArrayElements(env, out, p, rc < 0 ? JNI_ABORT : 0);
+    fail(env, rc);
+    return out;
+}
+
+/* per dense id: the minimum ORIGINAL id of its component (the reference's canonical form in signed Long order) */
+FN(jlongArray, canonical)(JNIEnv* env, jclass c, jlong h, jlong m) {
+    uint64_t n = 0;
+    if (fail(env, gcc_idmap_size(M(m), &n))) return 0;
+    uint32_t* lab = (uint32_t*)malloc((size_t)(n ? n : 1) * sizeof(uint32_t));
+    if (!lab) {
+        fail(env, GCC_E_OOM);
+        return 0;
+    }
+    int rc = gcc_forest_labels(H(h), lab, (uint32_t)n);
+    jlongArray out = 0;
+    if (rc >= 0) {
+        out = (*env)->NewLongArray(env, (jsize)n);
+        jlong* p = (*env)->GetLongArrayElements(env, out, 0);
+        rc = gcc_idmap_canonical(M(m), lab, n, (int64_t*)p, INT64_MIN);
+        (*env)->ReleaseLongArrayElements(env, out, p, rc < 0 ? JNI_ABORT : 0);
+    }
+    free(lab);
+    fail(env, rc);
+    return out;
+}

@@ -46,4 +46,24 @@ final class Gcc {
 
     /** gcc_forest_deserialize: fold serialized bytes into h. */
     static native void deserialize(long h, byte[] data);
+
+    // ---- Long vertex ids (gcc_idmap_*): DisjointSet<Long> takes any Long (DisjointSet.java:30-34) ----
+
+    /** gcc_idmap_create: a dictionary of at most `capacity` distinct ids (dense ids in first-seen order). */
+    static native long idmapCreate(int capacity);
+
+    /** gcc_idmap_destroy. */
+    static native void idmapDestroy(long m);
+
+    /** gcc_forest_staging + gcc_idmap_map into the slot + gcc_forest_submit: fold nPairs (Long, Long) pairs. */
+    static native void submitLong(long h, long m, long[] pairs, int nPairs);
+
+    /** gcc_idmap_lookup: the dense id of `id`, -1 if never mapped. */
+    static native int idmapLookup(long m, long id);
+
+    /** gcc_idmap_ids: original id of every dense id, in dense order. */
+    static native long[] idmapIds(long m);
+
+    /** gcc_forest_labels + gcc_idmap_canonical: per dense id, the minimum original id of its component. */
+    static native long[] canonical(long h, long m);
 }

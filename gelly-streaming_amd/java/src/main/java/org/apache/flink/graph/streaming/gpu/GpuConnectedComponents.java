@@ -15,7 +15,12 @@ public class GpuConnectedComponents extends SummaryBulkAggregation<Long, NullVal
     private static final long serialVersionUID = 1L;
 
     public GpuConnectedComponents(long mergeWindowTime, int device, int idCapacity) {
+        this(mergeWindowTime, device, idCapacity, false);
+    }
+
+    /** longIds: vertex ids are any Long (at most idCapacity distinct ones), mapped by the id dictionary. */
+    public GpuConnectedComponents(long mergeWindowTime, int device, int idCapacity, boolean longIds) {
         super(new ConnectedComponents.UpdateCC<Long>(), new ConnectedComponents.CombineCC<Long>(),
-                new GpuDisjointSet(device, idCapacity), mergeWindowTime, false);
+                new GpuDisjointSet(device, idCapacity, longIds), mergeWindowTime, false);
     }
 }

@@ -130,11 +130,14 @@ int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, u
 /* ---- cross-GPU merge message: the partial forest as the RCCL payload (replaces the Kryo-serialised
  * DisjointSet that SummaryBulkAggregation.java:81-83 ships to the one task running timeWindowAll.reduce).
  * Layout (one device buffer, gcc_msg_bytes(id_capacity, cap_others) bytes):
- *   u32 header[4] = { g, n_others, id_capacity, 0 }
+ *   u32 header[4] = { g, n_others, id_capacity, status }   status 0; GCC_MSG_STATUS_FAILED: the sender's merge
+ *                                          failed (header only, id_capacity 0: absorbed as nothing; every rank's
+ *                                          gcc_forest_group_merge then returns an error)
  *   u64 bits[ceil(id_capacity / 64)]      bit v set <=> label[v] == g   (g = the tracked giant's root)
  *   u32 others[2 * cap_others]            (v, label[v]) for every other seen v (n_others of them, any order)
  * The partition it encodes is exactly the forest's: {(v, g) : bit v} ∪ {(v, label[v]) : others}. */
 #define GCC_MSG_HEADER_BYTES 16
+#define GCC_MSG_STATUS_FAILED 1u
 uint64_t gcc_msg_bytes(uint32_t id_capacity, uint64_t cap_others);
 /* compress, then write the message into d_msg (async on h's stream); the header's n_others is the true
  * count even when it exceeds cap_others (then only cap_others entries are written: re-encode larger) */
@@ -214,6 +217,12 @@ int gcc_forest_serialized_size(gcc_forest* h, uint64_t* bytes);
 int gcc_forest_serialize(gcc_forest* h, void* out, uint64_t size, uint64_t* written);
 int gcc_forest_deserialize(gcc_forest* h, const void* in, uint64_t size);
 
+/* parity helper: compress (like gcc_forest_labels) and return, computed on the device, the digest of the canonical
+ * label array, sum over every id v of splitmix64((label[v] << 32) | v) mod 2^64 (GCC_UNSEEN labels included: the
+ * formula of tests/golden/stream_digests.json), plus #seen and #components (either pointer may be null).
+ * Synchronises. */
+int gcc_forest_label_digest(gcc_forest* h, uint64_t* digest, uint64_t* n_seen, uint64_t* n_components);
+
 /* ---- measurement: duration of the last fold launch (HIP events on the handle's stream) ---- */
 int gcc_forest_enable_timing(gcc_forest* h, int enable); /* 0 off, 1 events, 2 events + slow-edge counts */
 int gcc_forest_last_fold_ms(gcc_forest* h, float* ms);
@@ -221,6 +230,10 @@ int gcc_forest_last_fold_ms(gcc_forest* h, float* ms);
  * "phase ms edges" lines; each fold starts with a "begin" line (+ "slow_edges 0 n" lines in mode 2).
  * Recording never synchronises, so a timed region stays sync-free; this call synchronises. */
 int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size);
+/* diagnostics (tune key inc_check = 1): totals over this forest's checked incremental compresses: how many ran,
+ * labels that differed from the roots of the forest the compress started from, bloom words whose LDS copy lacked a
+ * mark that memory held. Checked compresses synchronise; never on in a timed region. */
+int gcc_forest_inc_check_stats(gcc_forest* h, uint64_t* checks, uint64_t* bad_labels, uint64_t* lost_marks);
 /* ---- id dictionary: Java Long vertex ids at the boundary (host-only, gelly_idmap.cpp) ----
  * DisjointSet<Long> (…/summaries/DisjointSet.java:30-34) is keyed by any Long; the device forest by dense u32
  * ids. The dictionary assigns dense ids in first-seen order and maps a forest's labels over dense ids back to
@@ -240,7 +253,7 @@ int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, 
 /* fold-pipeline tuning knobs; results never depend on them, only speed does. Keys: filter, filter_min_batch,
  * filter_min_share, sample_first, sample_growth, sample_div, sample_min, refresh_min_batch, refresh1..refresh3, depth, hook,
  * drain_at, seed, seed_nt, seed_global, seed_fuse, seed_passes, seed_div, seed_div1, seed_refresh, incremental,
- * inc_min_ids, inc_div, inc_inplace, refresh_labels, bucket, bucket_min_batch, bucket_min_ids, bucket_levels,
+ * inc_min_ids, inc_div, inc_inplace, inc_check (diagnostics), refresh_labels, bucket, bucket_min_batch, bucket_min_ids, bucket_levels,
  * bucket_sample, bucket_hub_sample, bucket_p1, bucket_slow2, bucket_defer, pin_chunk, lds_edges_per_word. Unknown keys return GCC_E_INVALID. */
 int gcc_forest_tune(gcc_forest* h, const char* key, double value);
 

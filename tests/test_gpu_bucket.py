@@ -269,3 +269,39 @@ def test_serialized_summary_rejects_bad_bytes():
         DisjointSet(1 << 5).deserialize(blob)  # larger id range than the target
     again = DisjointSet.from_bytes(blob)
     assert again.find(2) == 1 and again.find(4) == 3 and again.size() == 4
+
+
+def test_serialized_summary_rejects_wrapped_lengths():
+    """a kind-1 header whose n_seen makes 8 * n_seen wrap (2^61) with payload 0, and a payload that makes
+    header + payload wrap, must be rejected before any pair is read (GCC_E_INVALID), not folded past the buffer."""
+    import struct
+
+    V = 1 << 10
+    for n_seen, payload in ((1 << 61, 0), (4, (1 << 64) - 16), (3, 24 + 8)):
+        blob = struct.pack("<IIIIQQ", 0x53434347, 1, V, 1, n_seen, payload) + b"\x00" * 32
+        with pytest.raises(GellyCCError) as e:
+            DisjointSet(V).deserialize(blob)
+        assert e.value.code == -1, (n_seen, payload)
+
+
+def test_absorb_ignores_bitmap_bits_past_the_id_range(torch_cuda):
+    """a kind-2 (message) summary whose last bitmap word carries bits past id_capacity (untrusted bytes)
+    must not index parent[] out of range: those bits are masked, the rest of the message restores exactly."""
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], scale=17, n_edges=1 << 20, seed=0xB17)
+    E, V = cfg.info()
+    V = V - 7  # an id range that ends inside a 64-id bitmap word (and big enough for the giant filter)
+    pairs = G.generate_host(cfg) % np.uint32(V)
+    src = DisjointSet(V)
+    src.fold(pairs)
+    blob = bytearray(src.serialize())
+    hdr = np.frombuffer(bytes(blob[:32]), dtype="<u4")
+    assert hdr[3] == 2, "expected the message form (a dominant component)"
+    nw = (V + 63) // 64
+    last = 32 + 16 + 8 * (nw - 1)  # the message's last bitmap word
+    word = int.from_bytes(blob[last:last + 8], "little") | (~((1 << (V % 64)) - 1) & ((1 << 64) - 1))
+    blob[last:last + 8] = word.to_bytes(8, "little")
+    dst = DisjointSet(V)
+    dst.deserialize(bytes(blob))
+    assert np.array_equal(dst.labels(), src.labels())
+    src.close()
+    dst.close()

@@ -154,8 +154,9 @@ def test_rccl_comm_single_rank():
     comm = RcclComm(0, 1, 0, RcclComm.unique_id())
     ds = DisjointSet(1 << 12)
     ds.fold(np.array([[5, 6], [6, 9], [100, 101]], dtype=np.uint32))
+    assert ds.find(9) == 5  # caches the host labels
     comm.merge(ds)
-    ds._dirty()
+    assert ds._labels_cache is None  # RcclComm.merge drops the pre-merge view itself
     assert ds.find(9) == 5 and ds.find(101) == 100 and ds.size() == 5
     ds.close()
     comm.close()
