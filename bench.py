@@ -241,6 +241,9 @@ def make_roofline(kstats, phases, spans, inst_steps, workload, timing_note, host
     avg_fold_s = (sum(ms for ms, _ in spans) / len(spans) / 1e3) if spans else None
     avg_fold_edges = (sum(n for _, n in spans) / len(spans)) if spans else None
     pipeline_gbs = BYTES_PER_EDGE * avg_fold_edges / avg_fold_s / 1e9 if spans and avg_fold_s else None
+    # the whole step's measured HBM bytes (every kernel's PMC bytes x launches, per step; tools/pmc_summary.py)
+    pipe_prof = profile_record(workload)
+    pipe_traffic = pipe_prof.get("pipeline_traffic_per_step") if pipe_prof else None
     return {
         "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
@@ -254,7 +257,11 @@ def make_roofline(kstats, phases, spans, inst_steps, workload, timing_note, host
                      "edges_per_fold": int(avg_fold_edges) if avg_fold_edges else None,
                      "bytes_per_edge": BYTES_PER_EDGE, "achieved": pipeline_gbs,
                      "frac": (pipeline_gbs / HBM_PEAK_GBS) if pipeline_gbs else None,
-                     "host_enqueue_ms_avg": (sum(host_fold_s) / len(host_fold_s) * 1e3) if host_fold_s else None},
+                     "host_enqueue_ms_avg": (sum(host_fold_s) / len(host_fold_s) * 1e3) if host_fold_s else None,
+                     "traffic": pipe_traffic, "traffic_unit": "bytes per step",
+                     "traffic_ratio": (pipe_traffic / (BYTES_PER_EDGE * avg_fold_edges))
+                     if pipe_traffic and avg_fold_edges else None,
+                     "traffic_source": pipe_prof["file"] if pipe_traffic else None},
     }
 
 

@@ -30,9 +30,10 @@ constexpr int kP1Block = 512;
 constexpr int kP1Per = 16;                      // edges per thread per tile
 constexpr u32 kP1Tile = kP1Block * kP1Per;      // the smallest tile (bucket_applies: a batch of >= 2 tiles)
 constexpr int kP2Block = 1024;
-constexpr int kP2Per = 8;                       // edges per thread per round (4 x 16 B)
-constexpr u32 kP2Round = kP2Block * kP2Per;     // 8192 edges per round -> at most 8192 v's per LDS tile
-constexpr u32 kP2Tile = kP2Round + 3 * 256;     // + up to 3 padding slots per slice (kMaxSlicesLds)
+// P2 entries per thread per round (tune bucket_p2_per: 8 or 12): a round of kP2Block * PER entries, and at most that
+// many v's in the round's LDS tile + up to 3 padding slots per slice (kMaxSlicesLds)
+constexpr u32 p2_round(int per) { return (u32)kP2Block * per; }
+constexpr u32 p2_tile(int per) { return p2_round(per) + 3 * 256; }
 constexpr u32 kMaxSlicesLds = 256;              // LDS per-slice state: id ranges up to 2^27 (larger: the old path)
 constexpr int kP3Block = 1024;
 constexpr u32 kMaxP2Blocks = 1024;
@@ -90,6 +91,18 @@ __device__ __forceinline__ bool bk_decode(u32 lo, u16 hi, u32 sbase, u32& u, u32
     v = lo & kTgtMask;
     return hi != kPadHi;
 }
+
+// ---- v-list entries: 3 bytes (round 3; round 2 stored the u32 target). A v-list belongs to one target slice, so an
+// entry holds the target's 19 slice-local bits: lo (u16) = x[15:0], hi (u8) = x[18:16]; hi = 0xFF marks padding
+// or an unused chunk tail. P2 writes and P3 reads 3 B per listed edge instead of 4.
+typedef uint8_t u8;
+constexpr u8 kPadV = 0xFF;
+struct VList {
+    u16* lo;
+    u8* hi;
+};
+__host__ __device__ inline u64 vl_entries(u64 storage) { return (storage + 15) / 16 * 16; }
+__host__ __device__ inline u64 vl_bytes(u64 storage) { return 3 * vl_entries(storage); }
 
 // the bucket storage of S entries (S a multiple of 16): lo at the start, hi right after (16-B aligned)
 __host__ __device__ inline u64 bk_entries(u64 storage) { return (storage + 15) / 16 * 16; }
@@ -418,11 +431,11 @@ __device__ __forceinline__ void hook_g(u32* parent, u32 g, u32 v) {
 // SEG (second level, FINAL only): the items are the slow-list runs the FINAL pass recorded (`segs`, m->nseg of
 // them; `bk` = the slow array), C is then C | N, and its own slow edges go to `slow` (the bucket storage, free
 // by then). FINAL without SEG records those runs into `segs` (one per item with slow edges; null: none).
-template <bool FINAL, bool SEG = false>
+template <bool FINAL, bool SEG = false, int PER = 8>
 __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict__ parent, const u32* __restrict__ bk_lo,
                                                                 const u16* __restrict__ bk_hi, const u64* __restrict__ bk,
                                                                 const u32* __restrict__ bits, u32 nwords32, u32 ns,
-                                                                Meta* __restrict__ m, u32* __restrict__ vl, u32 cps,
+                                                                Meta* __restrict__ m, VList vl, u32 cps,
                                                                 u32 frac, u32 work_slot, u32 drain_at, u32 hub_only,
                                                                 const u32* __restrict__ giant, u64* __restrict__ slow,
                                                                 u32 slow_cap, u32 cap, u32* __restrict__ err,
@@ -431,8 +444,8 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     trace_start(FINAL ? kTrBkP2 : kTrBkP2Seed);
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     u32* s_bits = s_dyn;                                   // kSliceWords
-    u32* s_vt = s_dyn + kSliceWords;                       // kP2Tile: the round's targets + run padding
-    u32* s_cnt2 = s_vt + kP2Tile;                          // 2 x kMaxSlicesLds (double-buffered)
+    u32* s_vt = s_dyn + kSliceWords;                       // p2_tile(PER): the round's targets + run padding
+    u32* s_cnt2 = s_vt + p2_tile(PER);                          // 2 x kMaxSlicesLds (double-buffered)
     u32* s_pc = s_cnt2 + 2 * kMaxSlicesLds;                // kMaxSlicesLds: counts padded to 4
     u32* s_start = s_pc + kMaxSlicesLds;                   // kMaxSlicesLds
     u32* s_vcap = s_start + kMaxSlicesLds;                 // kMaxSlicesLds
@@ -441,7 +454,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     u64* ring = s_vbase + kMaxSlicesLds + (threadIdx.x >> 6) * kRing;  // FINAL only
     __shared__ u32 s_item, s_wsum[kP2Block / 64], s_slow;
     typedef u32 u4 __attribute__((ext_vector_type(4)));
-    constexpr int kQ = kP2Per / 2;
+    constexpr int kQ = PER / 2;
     const u32 lane = threadIdx.x & 63;
     const u32 g = FINAL ? *giant : 0u;
     u64* my_slow = slow + (u64)blockIdx.x * slow_cap;
@@ -520,8 +533,8 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         const u4* ep = reinterpret_cast<const u4*>(src) + plo;                        // SEG: pairs (16-B aligned)
         const u4* elo = reinterpret_cast<const u4*>(bk_lo + ebase) + plo;             // buckets: 16-B aligned
         const u64* ehi = reinterpret_cast<const u64*>(bk_hi + ebase) + plo;           // 8-B aligned
-        constexpr u32 kRoundItems = SEG ? kP2Round / 2 : kP2Round / 4;  // pairs or groups per round
-        constexpr int kL = SEG ? kQ : kP2Per / 4;                        // loads (of each stream) per thread
+        constexpr u32 kRoundItems = SEG ? p2_round(PER) / 2 : p2_round(PER) / 4;  // pairs or groups per round
+        constexpr int kL = SEG ? kQ : PER / 4;                        // loads (of each stream) per thread
         u4 q[kL];
         u64 qh[kL];
         auto load_round = [&](u32 p0) {
@@ -540,8 +553,8 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         load_round(0);
         for (u32 p0 = 0; p0 < np; p0 += kRoundItems) {
             u32* s_cnt = s_cnt2 + rb * kMaxSlicesLds;
-            u32 ua[kP2Per], va[kP2Per], rk[kP2Per];
-            bool in[kP2Per];
+            u32 ua[PER], va[PER], rk[PER];
+            bool in[PER];
             if constexpr (SEG) {
                 const bool skip_first = lo & 1, skip_last = hi & 1;  // the part starts / ends in the middle of a pair
 #pragma unroll
@@ -570,16 +583,16 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             }
             u32 bad = 0;
 #pragma unroll
-            for (int k = 0; k < kP2Per; ++k) {  // the target indexes global lists (v-lists, parent[]): < cap
+            for (int k = 0; k < PER; ++k) {  // the target indexes global lists (v-lists, parent[]): < cap
                 bad |= (u32)(in[k] && va[k] >= cap);
                 in[k] = in[k] && va[k] < cap;
             }
             if (bad) flag_err(err, kErrP2);
             if (p0 + kRoundItems < np) load_round(p0 + kRoundItems);  // next round in flight
-            bool emit[kP2Per];
+            bool emit[PER];
             u32 slow_m = 0;  // FINAL: this lane's slow edges (source not in C), bit k
 #pragma unroll
-            for (int k = 0; k < kP2Per; ++k) {
+            for (int k = 0; k < PER; ++k) {
                 const u32 iu = in[k] ? lds_bit(s_bits, ua[k] - sbase) : 0u;
                 emit[k] = in[k] && iu;
                 if (emit[k]) rk[k] = atomicAdd(&s_cnt[va[k] >> kSliceBits], 1u);
@@ -597,7 +610,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 base = __shfl(base, 63, 64);
                 u32 pos = base + incl - ns_l, spill_m = 0;
 #pragma unroll
-                for (int k = 0; k < kP2Per; ++k)
+                for (int k = 0; k < PER; ++k)
                     if ((slow_m >> k) & 1u) {
                         if (pos < slow_cap) my_slow[pos] = ((u64)va[k] << 32) | ua[k];
                         else spill_m |= 1u << k;
@@ -606,7 +619,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 if (__ballot(spill_m != 0)) {  // past the region (never at the default sizes): united right here
                     if (lane == 0) atomicOr(&m->ring_used, 1u);
 #pragma unroll
-                    for (int k = 0; k < kP2Per; ++k)
+                    for (int k = 0; k < PER; ++k)
                         ring_push((spill_m >> k) & 1u, ua[k], va[k], ring, wq, wd, parent, drain_at, 0xFFFFFFFFu);
                 }
             }
@@ -622,7 +635,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             }
             __syncthreads();  // (2) starts + reservations
 #pragma unroll
-            for (int k = 0; k < kP2Per; ++k)
+            for (int k = 0; k < PER; ++k)
                 if (emit[k]) s_vt[s_start[va[k] >> kSliceBits] + rk[k]] = va[k];
             __syncthreads();  // (3) tile in bucket order
             const u32 tot4 = (s_start[ns - 1] + s_pc[ns - 1]) / 4;
@@ -630,8 +643,13 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 const u4 v = reinterpret_cast<const u4*>(s_vt)[x4];  // slot 4 x4 is never padding
                 const u32 s = v.x >> kSliceBits;
                 const u32 off = run_pos(runs, s, 4 * x4 - s_start[s]);  // a multiple of 4: one chunk
-                if (off != 0xFFFFFFFFu) {
-                    *reinterpret_cast<u4*>(vl + s_vbase[s] + off) = v;  // 16-B aligned (bases: 16-entry multiples)
+                if (off != 0xFFFFFFFFu) {  // 8-B lo / 4-B hi stores (bases: 16-entry multiples, off: 4)
+                    const u16x4 lo = {(u16)v.x, (u16)v.y, (u16)v.z, (u16)v.w};
+                    const u32 hi = (v.x >> 16 & 7u) | (v.y == 0xFFFFFFFFu ? kPadV : (v.y >> 16 & 7u)) << 8 |
+                                   (v.z == 0xFFFFFFFFu ? kPadV : (v.z >> 16 & 7u)) << 16 |
+                                   (u32)(v.w == 0xFFFFFFFFu ? kPadV : (v.w >> 16 & 7u)) << 24;
+                    *reinterpret_cast<u16x4*>(vl.lo + s_vbase[s] + off) = lo;
+                    *reinterpret_cast<u32*>(vl.hi + s_vbase[s] + off) = hi;
                 } else if (FINAL) {  // the v-list is full: (u in C, v) = union(g, v) now
                     hook_g(parent, g, v.x);
                     if (v.y != 0xFFFFFFFFu) hook_g(parent, g, v.y);
@@ -645,7 +663,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     __syncthreads();
     // the unused tails of this block's chunks: UNSEEN (P3 skips them)
     for (u32 s = 0; s < ns; ++s)
-        for (u32 i = runs.cpos[s] + threadIdx.x; i < runs.cend[s]; i += kP2Block) vl[s_vbase[s] + i] = 0xFFFFFFFFu;
+        for (u32 i = runs.cpos[s] + threadIdx.x; i < runs.cend[s]; i += kP2Block) vl.hi[s_vbase[s] + i] = kPadV;
     if constexpr (FINAL) {  // the rest of this wave's ring; the block's slow count
         for (; wd < wq; wd += 64) {
             if (lane < wq - wd) {
@@ -667,12 +685,11 @@ constexpr int kP3Q = 4;
 template <bool FINAL>
 __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ bits, u32* __restrict__ out,
                                                               u32 nwords32, u32 ns, Meta* __restrict__ m,
-                                                              const u32* __restrict__ vl, u32 cps, u32 work_slot,
+                                                              VList vl, u32 cps, u32 work_slot,
                                                               u32 cap, u32* __restrict__ err) {
     trace_start(FINAL ? kTrBkP3 : kTrBkP3Seed);
     extern __shared__ __attribute__((aligned(16))) u32 s_bits[];  // kSliceWords
     __shared__ u32 s_item, s_min;
-    typedef u32 u4 __attribute__((ext_vector_type(4)));
     u32 cur_slice = 0xFFFFFFFFu;
     const u32 n_items = ns * cps;
     u32 lmin = 0xFFFFFFFFu;
@@ -684,13 +701,11 @@ __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ 
             if (nw && (!FINAL || (nw & ~out[w0 + w]))) atomicOr(&out[w0 + w], nw);
         }
     };
-    auto visit = [&](u32 v, u32 sbase) {
-        if (v == 0xFFFFFFFFu) return;  // a chunk tail (P2)
-        // (no range check: a v-list entry only indexes this block's LDS slice, never global memory)
-        const u32 x = v - sbase, msk = 1u << (x & 31);
+    auto visit = [&](u32 x, u32 sbase) {  // x: the slice-local target (19 bits: only indexes this block's LDS slice)
+        const u32 msk = 1u << (x & 31);
         if (s_bits[x >> 5] & msk) return;                  // already in C (or taken by this block)
         if (atomicOr(&s_bits[x >> 5], msk) & msk) return;  // another lane of the block took it
-        if (!FINAL) lmin = v < lmin ? v : lmin;
+        if (!FINAL) lmin = (sbase | x) < lmin ? (sbase | x) : lmin;
     };
     while (true) {
         __syncthreads();
@@ -710,25 +725,31 @@ __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ 
             cur_slice = sl;
             __syncthreads();
         }
-        const u32* v0 = vl + m->vl_base[sl];  // 16-B aligned
+        const u64* vlo = reinterpret_cast<const u64*>(vl.lo + m->vl_base[sl]);  // 4 entries per 8 B (aligned)
+        const u32* vhi = reinterpret_cast<const u32*>(vl.hi + m->vl_base[sl]);  // 4 entries per 4 B
         const u32 sbase = sl << kSliceBits;
         const u64 qlo = lo / 4, qhi = (hi + 3) / 4;  // 4-entry groups; entries outside [lo, hi) masked
         for (u64 b = qlo; b < qhi; b += (u64)kP3Q * kP3Block) {
-            u4 r[kP3Q];
+            u64 rl[kP3Q];
+            u32 rh[kP3Q];
 #pragma unroll
             for (int k = 0; k < kP3Q; ++k) {
                 const u64 j = b + (u64)k * kP3Block + threadIdx.x;
-                r[k] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(v0) + (j < qhi ? j : qhi - 1));
+                const u64 jc = j < qhi ? j : qhi - 1;  // clamped: countable loads
+                rl[k] = __builtin_nontemporal_load(vlo + jc);
+                rh[k] = __builtin_nontemporal_load(vhi + jc);
             }
 #pragma unroll
             for (int k = 0; k < kP3Q; ++k) {
                 const u64 j = b + (u64)k * kP3Block + threadIdx.x;
                 if (j >= qhi) continue;
                 const u64 e = 4 * j;
-                if (e >= lo && e < hi) visit(r[k].x, sbase);
-                if (e + 1 >= lo && e + 1 < hi) visit(r[k].y, sbase);
-                if (e + 2 >= lo && e + 2 < hi) visit(r[k].z, sbase);
-                if (e + 3 >= lo && e + 3 < hi) visit(r[k].w, sbase);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const u32 h8 = (rh[k] >> (8 * c)) & 0xFFu;
+                    if (h8 != kPadV && e + c >= lo && e + c < hi)  // padding: a P2 run pad or chunk tail
+                        visit((h8 << 16) | (u32)((rl[k] >> (16 * c)) & 0xFFFFu), sbase);
+                }
             }
         }
     }

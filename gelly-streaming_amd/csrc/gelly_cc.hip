@@ -1488,8 +1488,8 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
 
 #include "bucket_fold.h"
 
-static constexpr size_t slice_filter_lds() {  // bucket_fold.h slice_filter_kernel's dynamic LDS
-    return (bk::kSliceWords + bk::kP2Tile + 11 * bk::kMaxSlicesLds) * sizeof(u32) + bk::kMaxSlicesLds * sizeof(u64) +
+static constexpr size_t slice_filter_lds(int per = 8) {  // bucket_fold.h slice_filter_kernel's dynamic LDS
+    return (bk::kSliceWords + bk::p2_tile(per) + 11 * bk::kMaxSlicesLds) * sizeof(u32) + bk::kMaxSlicesLds * sizeof(u64) +
            (bk::kP2Block / 64) * kRing * sizeof(u64);
 }
 
@@ -1642,6 +1642,7 @@ struct FoldTune {
     int bucket_defer = 1;        // N labelled by the fold's closing compress instead of a store per id (bucket_join_kernel)
     int bucket_slow2 = 1;        // second filter level over the slow edges with C | N (C4's 1/8 share: 19 % slow edges)
     int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms)
+    int bucket_p2_per = 8;       // FINAL P2 entries per thread per round: 8 or 12 (fewer barriers per entry)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -1721,8 +1722,8 @@ struct gcc_forest {
     u64 bk_cap_bytes = 0;
     u64* d_ovf = nullptr;
     u64 ovf_cap = 0;
-    u32* d_vl = nullptr;
-    u64 vl_cap = 0;
+    uint8_t* d_vl = nullptr;  // v-lists: bk::vl_bytes(S) bytes = S 3-B entries (lo array, then hi array)
+    u64 vl_cap = 0;           // bytes
     u64* d_slow = nullptr;  // FINAL P2's slow edges, one region per block
     u64 slow_cap_total = 0;
     u32* d_nbits = nullptr;  // N: ids reached from C by the FINAL pass (kept all-zero between batches)
@@ -2216,7 +2217,9 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     u32* bk_lo = reinterpret_cast<u32*>(h->d_bk);
     bk::u16* bk_hi = reinterpret_cast<bk::u16*>(h->d_bk + 4 * bk_S);
     if ((rc = grow(h->d_ovf, h->ovf_cap, n / 8 + 65536, h->stream))) return rc;
-    if ((rc = grow(h->d_vl, h->vl_cap, bk::storage_edges(n, ns, p2_blocks), h->stream))) return rc;
+    const u64 vl_S = bk::vl_entries(bk::storage_edges(n, ns, p2_blocks));
+    if ((rc = grow(h->d_vl, h->vl_cap, bk::vl_bytes(vl_S), h->stream))) return rc;
+    const bk::VList vl{reinterpret_cast<bk::u16*>(h->d_vl), h->d_vl + 2 * vl_S};
     // room for half the batch in the slow lists (C4: 3.9 % slow; C4's 1/8 share: more than the 12.5 % an n/8
     // capacity held, and the rest took P2's inline ring unions: 1.03 ms instead of ~0.5)
     const u32 slow_cap = (u32)std::min<u64>(0x7FFFFFFEull, std::max<u64>(4096, n / p2_blocks / 2)) & ~1u;  // even: runs pair-aligned
@@ -2264,12 +2267,12 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
         rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
                       f_lds, h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,
-                      (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, l == 0 ? cps_hub : cps_seed, l == 0 ? frac_hub : frac, slot++, h->tune.drain_at, (u32)(l == 0),
+                      (const u32*)bits, nw32, ns, h->d_meta, vl, l == 0 ? cps_hub : cps_seed, l == 0 ? frac_hub : frac, slot++, h->tune.drain_at, (u32)(l == 0),
                       (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err,
                       (bk::SlowSeg*)nullptr);
         if (!rc)
             rc = launch_k(h, "seed_hook", 0, bk::slice_hook_kernel<false>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                          bits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps_seed, slot++, h->cap, h->d_err);
+                          bits, nw32, ns, h->d_meta, vl, cps_seed, slot++, h->cap, h->d_err);
     }
     // parent[] := C ? g : UNSEEN (the reset), then every bucketed edge, the overflow list, a spill
     if (!rc)
@@ -2277,13 +2280,16 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                       dim3(kBlock), 0, h->d_parent, h->cap, (const u32*)bits, (const bk::Meta*)h->d_meta, giant);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
-    rc = launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true>, dim3(p2_blocks), dim3(bk::kP2Block), f_lds,
-                  h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr, (const u32*)bits, nw32, ns,
-                  h->d_meta, h->d_vl, cps, 65536u, slot++,
-                  h->tune.drain_at, 0u, (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr);
+#define GCC_P2_FINAL(PER)                                                                                          \
+    launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true, false, PER>, dim3(p2_blocks), dim3(bk::kP2Block),    \
+             slice_filter_lds(PER), h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,       \
+             (const u32*)bits, nw32, ns, h->d_meta, vl, cps, 65536u, slot++, h->tune.drain_at, 0u, (const u32*)giant, \
+             h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr)
+    rc = t.bucket_p2_per == 12 ? GCC_P2_FINAL(12) : GCC_P2_FINAL(8);
+#undef GCC_P2_FINAL
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                      h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
+                      h->d_nbits, nw32, ns, h->d_meta, vl, cps, slot++, h->cap, h->d_err);
     const bool defer = t.bucket_defer != 0;
     if (!rc)
         rc = defer ? launch_k(h, "bucket_join", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
@@ -2301,11 +2307,11 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
         rc = launch_k(h, "slice_filter2", 0, bk::slice_filter_kernel<true, true>, dim3(p2_blocks), dim3(bk::kP2Block),
                       f_lds, h->d_parent, (const u32*)nullptr, (const bk::u16*)nullptr, (const u64*)h->d_slow,
-                      (const u32*)bits, nw32, ns, h->d_meta, h->d_vl, 1u, 65536u, slot++, h->tune.drain_at, 0u,
+                      (const u32*)bits, nw32, ns, h->d_meta, vl, 1u, 65536u, slot++, h->tune.drain_at, 0u,
                       (const u32*)giant, reinterpret_cast<u64*>(h->d_bk), slow_cap2, h->cap, h->d_err, h->d_seg);
         if (!rc)
             rc = launch_k(h, "slice_hook2", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                          h->d_nbits, nw32, ns, h->d_meta, (const u32*)h->d_vl, cps, slot++, h->cap, h->d_err);
+                          h->d_nbits, nw32, ns, h->d_meta, vl, cps, slot++, h->cap, h->d_err);
         if (!rc)
             rc = defer ? launch_k(h, "bucket_join2", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock),
                                   0, h->d_parent, bits, (const u32*)h->d_nbits, nw32, (const u32*)giant,
@@ -2665,6 +2671,7 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::slice_filter_kernel<false>, (int)slice_filter_lds()},
         {(const void*)bk::slice_filter_kernel<true>, (int)slice_filter_lds()},
         {(const void*)bk::slice_filter_kernel<true, true>, (int)slice_filter_lds()},
+        {(const void*)bk::slice_filter_kernel<true, false, 12>, (int)slice_filter_lds(12)},
         {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kSliceWords * sizeof(u32))},
         {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kSliceWords * sizeof(u32))},
         {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
@@ -3431,6 +3438,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "inc_check") t.inc_check = value != 0;
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = (int)value == 1 ? 1 : 0;
+    else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
     else if (k == "bucket_defer") t.bucket_defer = value != 0.0;
     else if (k == "bucket") t.bucket = value != 0;

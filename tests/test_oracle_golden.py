@@ -153,3 +153,23 @@ def test_label_digest_numpy_matches_c():
 
 def test_native_unseen_constant():
     assert native.UNSEEN == UNSEEN == orc.UNSEEN
+
+
+def test_windowed_digest_fixtures_are_consistent(golden):
+    """tests/golden/stream_digests.json's windowed entries (per-window parity at full size): the
+    windows tile the stream, their seen counts never shrink (union only grows), and the last window's summary is the
+    whole stream's (its own entry, computed in one window)."""
+    fx = golden("stream_digests.json")
+    windowed = [k for k in fx if "/w" in k]
+    assert {"c4_kron26/w8", "c3_gnm24/w4M", "c3_gnm24/w1M", "c5_adversarial/w64K"} <= set(windowed)
+    for k in windowed:
+        e = fx[k]
+        whole = fx[e["config"]]
+        ends = [w["end"] for w in e["windows"]]
+        assert ends == sorted(ends) and ends[-1] == e["edges"] == whole["edges"], k
+        assert all(b - a <= e["window_edges"] for a, b in zip([0] + ends, ends)), k
+        seen = [w["seen"] for w in e["windows"]]
+        assert seen == sorted(seen), k
+        last = e["windows"][-1]
+        assert (last["digest"], last["seen"], last["components"]) == (whole["digest"], whole["seen"],
+                                                                      whole["components"]), k

@@ -52,6 +52,15 @@ def main():
     rec["all_kernels"] = {  # every kernel of the run: HBM bytes per launch (same correction)
         k: {"launches": len(f[k]), "hbm_bytes_per_launch": (2 * sum(f[k]) / len(f[k]) + (sum(w[k]) / len(w[k]) if w.get(k) else 0)) * 1024}
         for k in f}
+    # the whole step's HBM traffic: every kernel of the run except the generator and the label copies, per step
+    # (steps = the dominant kernel's launches: one per step; run bench with --no-extras so no other leg is counted)
+    steps = len(fv) / max(1, len(names))
+    skip = ("gen_kernel", "__amd_rocclr_copyBuffer")
+    per_step = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in rec["all_kernels"].items()
+                   if not any(x in k for x in skip)) / max(1.0, steps)
+    rec["pipeline_traffic_per_step"] = per_step
+    rec["pipeline_algorithmic_per_step"] = 16.0 * edges
+    rec["pipeline_traffic_ratio"] = per_step / (16.0 * edges)
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
