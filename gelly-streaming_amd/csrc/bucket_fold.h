@@ -240,14 +240,16 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     }
 }
 
-// Block-wide exclusive scan of cnt[0..ns) into start[]; returns nothing (BLOCK threads, ns <= kMaxSlicesLds).
+// Block-wide exclusive scan of the counts cnt[0..ns), each rounded up to a multiple of 4 (pad4: the runs' padded
+// lengths), into start[] (BLOCK threads, ns <= kMaxSlicesLds). One barrier inside.
+__device__ __forceinline__ u32 pad4(u32 c) { return (c + 3) & ~3u; }
 template <int BLOCK>
 __device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u32* s_wsum) {
     const u32 per = (ns + BLOCK - 1) / BLOCK;
     u32 loc = 0;
     for (u32 j = 0; j < per; ++j) {
         const u32 s = threadIdx.x * per + j;
-        loc += s < ns ? cnt[s] : 0;
+        loc += s < ns ? pad4(cnt[s]) : 0;
     }
     const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     u32 inc = loc;
@@ -263,7 +265,7 @@ __device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u
         const u32 s = threadIdx.x * per + j;
         if (s < ns) {
             start[s] = run;
-            run += cnt[s];
+            run += pad4(cnt[s]);
         }
     }
 }
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
     // the tile in bucket order: dynamic LDS (p1_lds: P1B * P1P + kMaxSlicesLds u64, 66 / 130 KiB), set up like every
     // kernel's LDS beyond 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-slice state below is static
     extern __shared__ __attribute__((aligned(16))) u64 s_srt[];
-    __shared__ u32 s_cnt[kMaxSlicesLds], s_pc[kMaxSlicesLds], s_start[kMaxSlicesLds], s_cap[kMaxSlicesLds];
+    __shared__ u32 s_cnt[kMaxSlicesLds], s_start[kMaxSlicesLds], s_cap[kMaxSlicesLds];
     __shared__ u32 s_cpos[kMaxSlicesLds], s_cend[kMaxSlicesLds], s_p1[kMaxSlicesLds], s_l1[kMaxSlicesLds],
         s_p2[kMaxSlicesLds], s_l2[kMaxSlicesLds];
     __shared__ u64 s_base[kMaxSlicesLds];
@@ -350,19 +352,18 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
         __syncthreads();  // the tile's counts are complete
         // every bucket's run is padded to a multiple of 4 with ~0 entries (P2 skips them), so that runs, tile
         // slots and list positions stay multiples of 4 and the write-out moves 4 entries per lane (16 B of lo, 8 of hi)
-        for (u32 s = threadIdx.x; s < ns; s += P1B) s_pc[s] = (s_cnt[s] + 3) & ~3u;
-        __syncthreads();
-        count_scan<P1B>(s_pc, s_start, ns, s_wsum);
+        count_scan<P1B>(s_cnt, s_start, ns, s_wsum);
         for (u32 s = threadIdx.x; s < ns; s += P1B) {
-            if (s_pc[s]) reserve_run(runs, s, s_pc[s], &m->bk_cur[s], s_cap[s]);
-            for (u32 j = s_cnt[s]; j < s_pc[s]; ++j) s_srt[s_start[s] + j] = ~0ull;
+            const u32 pc = pad4(s_cnt[s]);
+            if (pc) reserve_run(runs, s, pc, &m->bk_cur[s], s_cap[s]);
+            for (u32 j = s_cnt[s]; j < pc; ++j) s_srt[s_start[s] + j] = ~0ull;
         }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < P1P; ++k)
             if (ok[k]) s_srt[s_start[ua[k] >> kSliceBits] + rk[k]] = ((u64)va[k] << 32) | ua[k];
         __syncthreads();
-        const u32 tot4 = (s_start[ns - 1] + s_pc[ns - 1]) / 4;
+        const u32 tot4 = (s_start[ns - 1] + pad4(s_cnt[ns - 1])) / 4;
         for (u32 x4 = threadIdx.x; x4 < tot4; x4 += P1B) {
             const u64x2 ea = reinterpret_cast<const u64x2*>(s_srt)[2 * x4];      // slot 4 x4 is never padding
             const u64x2 eb = reinterpret_cast<const u64x2*>(s_srt)[2 * x4 + 1];
@@ -624,13 +625,12 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 }
             }
             __syncthreads();  // (1) counts of this round complete
-            // runs padded to a multiple of 4 with UNSEEN (P3 skips it): a lane writes 4 targets per 16-B store
-            for (u32 s = threadIdx.x; s < ns; s += kP2Block) s_pc[s] = (s_cnt[s] + 3) & ~3u;
-            __syncthreads();
-            count_scan<kP2Block>(s_pc, s_start, ns, s_wsum);
+            // runs padded to a multiple of 4 with UNSEEN (P3 skips it): a lane writes 4 targets per store
+            count_scan<kP2Block>(s_cnt, s_start, ns, s_wsum);
             for (u32 s = threadIdx.x; s < ns; s += kP2Block) {
-                if (s_pc[s]) reserve_run(runs, s, s_pc[s], &m->vl_cur[s], s_vcap[s]);
-                for (u32 j = s_cnt[s]; j < s_pc[s]; ++j) s_vt[s_start[s] + j] = 0xFFFFFFFFu;
+                const u32 pc = pad4(s_cnt[s]);
+                if (pc) reserve_run(runs, s, pc, &m->vl_cur[s], s_vcap[s]);
+                for (u32 j = s_cnt[s]; j < pc; ++j) s_vt[s_start[s] + j] = 0xFFFFFFFFu;
                 s_cnt2[(rb ^ 1) * kMaxSlicesLds + s] = 0;  // the next round's buffer
             }
             __syncthreads();  // (2) starts + reservations
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             for (int k = 0; k < PER; ++k)
                 if (emit[k]) s_vt[s_start[va[k] >> kSliceBits] + rk[k]] = va[k];
             __syncthreads();  // (3) tile in bucket order
-            const u32 tot4 = (s_start[ns - 1] + s_pc[ns - 1]) / 4;
+            const u32 tot4 = (s_start[ns - 1] + pad4(s_cnt[ns - 1])) / 4;
             for (u32 x4 = threadIdx.x; x4 < tot4; x4 += kP2Block) {
                 const u4 v = reinterpret_cast<const u4*>(s_vt)[x4];  // slot 4 x4 is never padding
                 const u32 s = v.x >> kSliceBits;

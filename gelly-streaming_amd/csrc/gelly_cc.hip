@@ -1619,10 +1619,11 @@ struct FoldTune {
     bool incremental = true;
     bool inc_inplace = true;  // the incremental compress rewrites only changed parent[] slots (no spare buffer)
     u64 inc_min_ids = 1ull << 22;
-    // 64, not 8 (round 2): a batch of 1/16 of the ids (C3's last 1M-edge window, ~500K hooks) fills the 1M-bit bloom
-    // to a ~60 % false-hit rate, so the incremental compress walks for most ids anyway; and in two full-suite runs
-    // that window's incremental compress left ONE label stale (not root-caused). C5 (1/256) keeps it.
-    u64 inc_div = 64;
+    // chosen by speed (round 3, tools/sweep_inc_div.py, profiles/r3c_sweep_inc_div.log): on C3 and C5 the recording
+    // fold + incremental compress beat the plain fold + full compress at every window size up to 1/4 of the ids
+    // (C3 at 1/4: 555 vs 574 us per window; at 1/16: 170 vs 214). Round 2 had raised it to 64 after a stale label
+    // it could not explain; round 3's hardware probe and in-library checks did not reproduce it.
+    u64 inc_div = 4;
     // diagnostics: every incremental compress is checked against the roots of the forest it started from and its
     // bloom LDS copies against memory-side reads; failures go to stderr and to gcc_forest_inc_check_stats
     bool inc_check = false;
@@ -1641,8 +1642,10 @@ struct FoldTune {
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
     int bucket_defer = 1;        // N labelled by the fold's closing compress instead of a store per id (bucket_join_kernel)
     int bucket_slow2 = 1;        // second filter level over the slow edges with C | N (C4's 1/8 share: 19 % slow edges)
-    int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms)
-    int bucket_p2_per = 8;       // FINAL P2 entries per thread per round: 8 or 12 (fewer barriers per entry)
+    int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms), 2 = 1024 x 12
+    // FINAL P2 entries per thread per round: 8 or 12 (fewer barriers per entry; C4: P2 3.73 -> 3.23 ms,
+    // profiles/r3c_ab_p2_per.log)
+    int bucket_p2_per = 12;
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -2253,6 +2256,9 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         rc = t.bucket_p1 == 1
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16>, dim3(h->n_cu), dim3(1024), bk::p1_lds(1024, 16),
                             edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err)
+             : t.bucket_p1 == 2
+                 ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 12>, dim3(h->n_cu), dim3(1024), bk::p1_lds(1024, 12),
+                            edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err)
                  : launch_k(h, "bucket", n, bk::bucket_kernel<512, 16>, dim3(p1_blocks), dim3(512), bk::p1_lds(512, 16),
                             edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err);
     if (rc) return rc;
@@ -2677,6 +2683,7 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
         {(const void*)bk::bucket_kernel<512, 16>, (int)bk::p1_lds(512, 16)},
         {(const void*)bk::bucket_kernel<1024, 16>, (int)bk::p1_lds(1024, 16)},
+        {(const void*)bk::bucket_kernel<1024, 12>, (int)bk::p1_lds(1024, 12)},
     };
     for (const auto& t : tab) HIP_TRY(hipFuncSetAttribute(t.f, hipFuncAttributeMaxDynamicSharedMemorySize, t.bytes));
     return set_trace_slot();
@@ -3437,7 +3444,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "inc_div") t.inc_div = std::max<u64>(1, (u64)value);
     else if (k == "inc_check") t.inc_check = value != 0;
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
-    else if (k == "bucket_p1") t.bucket_p1 = (int)value == 1 ? 1 : 0;
+    else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(2, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
     else if (k == "bucket_defer") t.bucket_defer = value != 0.0;

@@ -553,6 +553,8 @@ KNOB_CASES = {
     "bucket_defer": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_defer": 0},
     "bucket_hub_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_hub_sample": 0.1},
     "lds_edges_per_word": {"lds_edges_per_word": 1e9},  # the short windows take the global-bitmap filter
+    "bucket_p2_per": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 12},
+    "inc_check": {"inc_min_ids": 1024, "inc_div": 1, "inc_check": 1},  # diagnostics: checks every incremental compress
 }
 
 
