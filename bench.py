@@ -40,11 +40,13 @@ KERNEL_BYTES = {
     "compress_inc_kernel": (8.125, "id"),   # the same, incremental (bloom of the window's mutations in LDS)
     "seed_pack_kernel": (5.125, "id"),      # flag byte read + parent write + 1 bitmap bit (the init variant)
     "seed_hub_kernel": (1.125, "id"),       # flag byte + bitmap bit cleared
-    "bucket_kernel": (16, "edge"),          # read the edge + write it into its u-slice bucket
-    "slice_filter_kernel<true>": (12, "edge"),   # FINAL P2: read the bucketed edge + write v of u-in-C edges (4 B)
-    "slice_filter_kernel<false>": (12, "edge"),  # a seeding level's P2 over the bucket samples
-    "slice_hook_kernel<true>": (4, "edge"),      # FINAL P3: read the v-lists (units: the batch's edges)
-    "slice_hook_kernel<false>": (4, "edge"),     # a seeding level's P3
+    # the bucketed fold's P1 runs over every edge of the batch once: priced at SURVEY §8(d)'s 16 B per edge (its own
+    # traffic is 8 B read + 6 B bucket entry written, round 3)
+    "bucket_kernel": (16, "edge"),
+    "slice_filter_kernel<true>": (9, "edge"),    # FINAL P2: read the 6-B bucket entry + write the 3-B v-list entry
+    "slice_filter_kernel<false>": (9, "edge"),   # a seeding level's P2 over the bucket samples
+    "slice_hook_kernel<true>": (3, "edge"),      # FINAL P3: read the 3-B v-list entries (units: the batch's edges)
+    "slice_hook_kernel<false>": (3, "edge"),     # a seeding level's P3
     "bucket_init_kernel": (4.125, "id"),    # parent write + 1 bitmap bit
 }
 C2_BATCHES = 4  # rotating C2 batches (tests/golden/stream_digests.json c2_rmat20@k)

@@ -634,10 +634,14 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
 // `bloom` (fold_kernel<true>; uf_device.h explains why an unmarked parent is still a root). labels[v] = p =
 // parent[v] unless p is marked, and only then a (read-only) find. So the pass is a coalesced stream of parent[]
 // and labels[] instead of a random read of parent[p] per seen non-root. One 1024-thread block per CU holds the
-// bloom in LDS; a lane reads 4 consecutive ids (16 B) and a wave covers 256 ids = 4 bitmap words of the
-// tracked component (as compress_bits_kernel). The block also clears its share of the other bloom buffer.
+// bloom in LDS; a wave covers 256 ids = 4 bitmap words of the tracked component per chunk, lane l the ids 64 j + l.
+// The block also clears its share of the other bloom buffer.
 constexpr int kIncBlock = 1024;
-constexpr int kIncU = 2;  // 256-id chunks per wave per batch (A/B: 2 beat 1, 4 and 8 on C5; profiles/r2_ab_chunk_batches.log)
+#ifndef GCC_INC_U  // A/B builds only (tools/gpu_c5.sh)
+#define GCC_INC_U 2
+#endif
+constexpr int kIncU = GCC_INC_U;  // 256-id chunks per wave per batch (A/B: 2 beat 1, 4 and 8 on C5; profiles/r2_ab_chunk_batches.log)
+constexpr int kIncQ = 128;  // queued finds per wave (two per lane per flush): 16 KiB of LDS beside the 128 KiB bloom
 using gcc::inc_label;  // uf_device.h: shared with the host replay
 
 // INPLACE: labels == parent. parent[] is already canonical except where a marked parent needs the find, so only
@@ -658,19 +662,24 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
     trace_start(kTrCompressInc);
     extern __shared__ __attribute__((aligned(16))) u32 s_bloom[];
     __shared__ u32 s_g;
+    __shared__ u32 s_qv[kIncBlock / 64][kIncQ], s_qp[kIncBlock / 64][kIncQ];  // queued finds per wave: id, parent
     constexpr u32 kW4 = gcc::kBloomBits / 128;  // bloom size in 16-B words
     const u32 lane = threadIdx.x & 63;
     const u64 nwords = ((u64)n + 63) / 64;
     const u64 nfull = (u64)n / 256;  // whole 256-id chunks (one 16-B load per lane); the partial tail: below
     const u64 nwaves = (u64)gridDim.x * (kIncBlock / 64);
     const u64 wave = (u64)blockIdx.x * (kIncBlock / 64) + (threadIdx.x >> 6);
-    // the first batch of parent[] loads is issued before the bloom's LDS fill and lands behind it
-    u32x4 pv[kIncU];
+    // the first batch of parent[] loads is issued before the bloom's LDS fill and lands behind it. Lane l of a wave
+    // takes ids 64 j + l (j < 4) of each 256-id chunk: four coalesced 256-B loads per chunk, and a ballot over the
+    // wave of one predicate per j is then the chunk's bitmap word j itself (no cross-lane shuffles)
+    u32 pv[kIncU][4];
     auto load_batch = [&](u64 base) {
 #pragma unroll
         for (int k = 0; k < kIncU; ++k) {  // clamped, unconditional: the compiler can count them
             const u64 ch = base + (u64)k * nwaves;
-            pv[k] = *reinterpret_cast<const u32x4*>(parent + (ch < nfull ? ch : nfull - 1) * 256 + 4 * lane);
+            const u32* src = parent + (ch < nfull ? ch : nfull - 1) * 256 + lane;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pv[k][j] = src[64 * j];
         }
     };
     if (wave < nfull) load_batch(wave);
@@ -707,37 +716,103 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
         }
     }
     const u32 g = s_g;
-    // kIncU chunks per wave in flight (one 16-B load each) before any is labelled: a wave that waited for each
-    // chunk in turn kept ~4 MB in flight device-wide and streamed C5's 64 MB parent[] at ~2.2 TB/s
+    // The ids whose parent is marked need a find: a chain of dependent loads. Walked inline (inc_label), each hop
+    // waited for every load in flight (vmcnt is in order), the next batch's prefetch included, and with 512 ids
+    // per wave per batch almost every batch of C5 had a marked parent somewhere. So the stream only labels the
+    // unmarked ids (their label is the parent: nothing to store in place), writes the bitmap words from them, and
+    // queues the marked ones per wave in LDS; a flush walks up to kIncQ queued finds at once (two chains per lane
+    // in lock step), stores their roots and ORs their bits into the words already written. The flush's fences
+    // order those stores after the stream's stores to the same words / slots (other lanes of the same wave).
+    const u32 wv = threadIdx.x >> 6;
+    u32 qn = 0;  // queued finds of this wave (wave-uniform)
+    auto order = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    auto settle = [&](u32 v, u32 p, u32 r) {  // a resolved find: the label and the tracked component's bit
+        if (!INPLACE || r != p) labels[v] = r;
+        if (r == g) __hip_atomic_fetch_or(bits + (v >> 6), 1ull << (v & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto flush = [&]() {
+        order();
+        const bool ha = lane < qn, hb = lane + 64 < qn;
+        const u32 va = ha ? s_qv[wv][lane] : 0, pa = ha ? s_qp[wv][lane] : 0;
+        const u32 vb = hb ? s_qv[wv][lane + 64] : 0, pb = hb ? s_qp[wv][lane + 64] : 0;
+        u32 ra = pa, rb = pb;  // an idle chain starts at 0: parent[0] is 0 or UNSEEN, never below it
+        for (;;) {
+            const u32 na = parent[ra], nb = parent[rb];
+            const bool ma = na < ra, mb = nb < rb;
+            if (!ma && !mb) break;
+            if (ma) ra = na;
+            if (mb) rb = nb;
+        }
+        if (ha) settle(va, pa, ra);
+        if (hb) settle(vb, pb, rb);
+        qn = 0;
+    };
+    const u64 lt = (1ull << lane) - 1;
+    const bool track = g != UNSEEN;  // no tracked component: no bit is set
+    // kIncU chunks per wave in flight before any is labelled: a wave that waited for each chunk in turn kept ~4 MB
+    // in flight device-wide and streamed C5's 64 MB parent[] at ~2.2 TB/s
     for (u64 base = wave; base < nfull; base += (u64)kIncU * nwaves) {
-        u32x4 cur[kIncU];
+        u32 cur[kIncU][4];
 #pragma unroll
-        for (int k = 0; k < kIncU; ++k) cur[k] = pv[k];
+        for (int k = 0; k < kIncU; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cur[k][j] = pv[k][j];
         const u64 nb = base + (u64)kIncU * nwaves;
         if (nb < nfull) load_batch(nb);  // wave-uniform: the next batch streams in while this one is labelled
 #pragma unroll
         for (int k = 0; k < kIncU; ++k) {
             const u64 ch = base + (u64)k * nwaves;
             if (ch >= nfull) break;  // wave-uniform
-            const u64 v0 = ch * 256 + 4 * lane;
-            const u32x4 p = cur[k];
-            u32 lab[4];
-            lab[0] = inc_label(parent, s_bloom, (u32)v0, p.x);
-            lab[1] = inc_label(parent, s_bloom, (u32)v0 + 1, p.y);
-            lab[2] = inc_label(parent, s_bloom, (u32)v0 + 2, p.z);
-            lab[3] = inc_label(parent, s_bloom, (u32)v0 + 3, p.w);
-            if constexpr (INPLACE) {
-                if (lab[0] != p.x) labels[v0] = lab[0];
-                if (lab[1] != p.y) labels[v0 + 1] = lab[1];
-                if (lab[2] != p.z) labels[v0 + 2] = lab[2];
-                if (lab[3] != p.w) labels[v0 + 3] = lab[3];
-            } else {
-                const u32x4 o = {lab[0], lab[1], lab[2], lab[3]};
-                *reinterpret_cast<u32x4*>(labels + v0) = o;
+            const u32 v0 = (u32)(ch * 256) + lane;  // this lane's ids: v0 + 64 j
+            // branch-free: every id reads its bloom word (roots and UNSEEN too), the four LDS reads in flight
+            // together (a short-circuit test compiled to a branch and a wait per id)
+            u32 bw[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bw[j] = s_bloom[gcc::bloom_word(cur[k][j])];
+            u32 dm = 0;
+            u64 wd[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u32 p = cur[k][j];
+                const u32 m = gcc::bloom_mask(p);
+                const bool d = (p < v0 + 64 * j) & ((bw[j] & m) == m);
+                dm |= (u32)d << j;
+                wd[j] = __ballot(!d && p == g && track);
+                if constexpr (!INPLACE) labels[v0 + 64 * j] = p;  // marked slots: rewritten by the flush
             }
-            chunk_bits(bits, nwords, ch, lane, g, lab);
+            if (lane < 4) bits[ch * 4 + lane] = lane == 0 ? wd[0] : lane == 1 ? wd[1] : lane == 2 ? wd[2] : wd[3];
+            if (__ballot(dm != 0) == 0) continue;  // wave-uniform: the common chunk
+            const u32 cnt = __popc(dm);
+            const u64 b1 = __ballot(cnt & 1), b2 = __ballot(cnt & 2), b4 = __ballot(cnt & 4);
+            const u32 tot = __popcll(b1) + 2 * __popcll(b2) + 4 * __popcll(b4);
+            if (qn + tot > (u32)kIncQ) flush();
+            if (tot > (u32)kIncQ) {  // a dense chunk: its finds inline
+                order();
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if ((dm >> j) & 1u) {
+                        NoCount c;
+                        const u32 v = v0 + 64 * j;
+                        settle(v, cur[k][j], UFRead::find_from(const_cast<u32*>(parent), v, cur[k][j], c));
+                    }
+                continue;
+            }
+            u32 pos = qn + __popcll(b1 & lt) + 2 * __popcll(b2 & lt) + 4 * __popcll(b4 & lt);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((dm >> j) & 1u) {
+                    s_qv[wv][pos] = v0 + 64 * j;
+                    s_qp[wv][pos] = cur[k][j];
+                    ++pos;
+                }
+            qn += tot;
         }
     }
+    if (qn) flush();
     if (nfull * 256 < n && wave == nfull % nwaves) {  // the partial last chunk: id by id
         const u64 v0 = nfull * 256 + 4 * lane;
         u32 lab[4] = {UNSEEN, UNSEEN, UNSEEN, UNSEEN};

@@ -129,20 +129,20 @@ struct Count {
 // p that is some id's parent is still a root: that id's label is p, no find needed. Ids that leave UNSEEN need
 // no mark: one hung straight under a root never becomes a parent value, one made a root is marked if hooked.
 constexpr u32 kBloomBits = 1u << 20;  // 128 KiB: one CU's LDS copy in the incremental compress
-// A BLOCKED bloom filter (round 3): a mark sets kBloomK bits of ONE 32-bit word (the word and the bits from two
-// independent hashes), so marking is one memory-side atomicOr and a test one LDS read. Round 2's filter set 2 bits
+// A BLOCKED bloom filter (round 3): a mark sets kBloomK bits of ONE 32-bit word, so marking is one memory-side
+// atomicOr and a test one LDS read. Round 2's filter set 2 bits
 // in 2 words: two atomics per hook in the fold (the fold of a short window is bound by memory-side atomics) and a
 // 1.4 % false-hit rate at C5's 65K marks per window; 4 bits in one of 32K words: ~0.8 %.
-constexpr int kBloomK = 4;
-UF_HD u32 bloom_word(u32 x) { return (x * 0x9E3779B1u) >> 17; }  // 15 bits: one of kBloomBits / 32 words
+// One multiply per test (round 3): the incremental compress tests every id of the forest, and with three 32-bit
+// multiplies per test (a quarter-rate VALU op each) it was bound by the VALU, not by its 16-B stream. The word is
+// the product's top 15 bits and the kBloomK bit positions its next 15 bits (5 each); bit i of x * K depends on bits
+// 0..i of x only, so the low 2 bits are left out.
+constexpr int kBloomK = 3;
+constexpr u32 kBloomMul = 0x9E3779B1u;
+UF_HD u32 bloom_word(u32 x) { return (x * kBloomMul) >> 17; }  // 15 bits: one of kBloomBits / 32 words
 UF_HD u32 bloom_mask(u32 x) {
-    u32 h = x * 0x85EBCA77u;
-    h ^= h >> 15;
-    h *= 0xC2B2AE3Du;
-    u32 m = 0;
-    UF_UNROLL
-    for (int i = 0; i < kBloomK; ++i) m |= 1u << ((h >> (27 - 5 * i)) & 31);
-    return m;
+    const u32 h = x * kBloomMul;
+    return (1u << ((h >> 12) & 31)) | (1u << ((h >> 7) & 31)) | (1u << ((h >> 2) & 31));
 }
 UF_HD bool bloom_test(const u32* bloom, u32 x) {
     const u32 m = bloom_mask(x);
