@@ -64,6 +64,34 @@ struct SlowSeg {
 };
 
 __device__ __forceinline__ u32 lds_bit(const u32* s, u32 x) { return (s[x >> 5] >> (x & 31)) & 1u; }
+
+// Phase timing (diagnostic builds only: -DGCC_PHASES): thread 0 of every block accumulates clock64() deltas per
+// phase of P1's tile loop (kernel 0) and FINAL P2's round loop (kernel 1); GELLY_BUCKET_STATS prints them.
+#ifdef GCC_PHASES
+__device__ unsigned long long gcc_phase_acc[2][16];
+struct PhaseClock {
+    unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long t = 0;
+    __device__ __forceinline__ void start() { t = clock64(); }
+    __device__ __forceinline__ void mark(int k) {
+        const unsigned long long n = clock64();
+        acc[k] += n - t;
+        t = n;
+    }
+    __device__ __forceinline__ void flush(int kern) {
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 8; ++k) atomicAdd(&gcc_phase_acc[kern][k], acc[k]);
+    }
+};
+#define GCC_PH_START(pc) (pc).start()
+#define GCC_PH_MARK(pc, k) (pc).mark(k)
+#define GCC_PH_FLUSH(pc, kern) (pc).flush(kern)
+#else
+struct PhaseClock {};
+#define GCC_PH_START(pc) (void)0
+#define GCC_PH_MARK(pc, k) (void)0
+#define GCC_PH_FLUSH(pc, kern) (void)0
+#endif
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t u16;
 typedef u16 u16x4 __attribute__((ext_vector_type(4)));
@@ -124,7 +152,10 @@ constexpr u32 kSlack = 1u << 12;
 // Writers reserve space in a bucket / v-list a CHUNK at a time per (block, slice) — one global atomic per chunk,
 // not per tile — and mark the unused tail of their last chunk with UNSEEN at exit (readers skip UNSEEN entries).
 // Each list's capacity therefore carries one chunk per writing block of slack.
-constexpr u32 kChunk = 1024;
+#ifndef GCC_KCHUNK
+#define GCC_KCHUNK 1024
+#endif
+constexpr u32 kChunk = GCC_KCHUNK;
 
 __host__ __device__ inline u64 storage_edges(u64 n, u32 ns, u32 blocks) {
     return n + n / 4 + (u64)ns * (kSlack + 64 + (u64)blocks * kChunk) + 64;
@@ -329,6 +360,8 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
     u4 q[kQ];
     u64 t = blockIdx.x;
     if (t < ntiles) load_tile(t, q);
+    [[maybe_unused]] PhaseClock phc;
+    GCC_PH_START(phc);
     for (; t < ntiles; t += gridDim.x) {
         for (u32 s = threadIdx.x; s < ns; s += P1B) s_cnt[s] = 0;
         u32 ua[P1P], va[P1P], rk[P1P];
@@ -343,13 +376,17 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
             ok[2 * k] = ok[2 * k + 1] = j < n2;
         }
         if (t + gridDim.x < ntiles) load_tile(t + gridDim.x, q);  // the next tile streams in meanwhile
+        GCC_PH_MARK(phc, 0);  // waited for this tile's loads
         __syncthreads();
+        GCC_PH_MARK(phc, 1);
 #pragma unroll
         for (int k = 0; k < P1P; ++k) {
             if (ok[k]) ok[k] = edge_ok(ua[k], va[k], cap, err);
             if (ok[k]) rk[k] = atomicAdd(&s_cnt[ua[k] >> kSliceBits], 1u);
         }
+        GCC_PH_MARK(phc, 2);  // LDS counting
         __syncthreads();  // the tile's counts are complete
+        GCC_PH_MARK(phc, 3);
         // every bucket's run is padded to a multiple of 4 with ~0 entries (P2 skips them), so that runs, tile
         // slots and list positions stay multiples of 4 and the write-out moves 4 entries per lane (16 B of lo, 8 of hi)
         count_scan<P1B>(s_cnt, s_start, ns, s_wsum);
@@ -359,10 +396,13 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
             for (u32 j = s_cnt[s]; j < pc; ++j) s_srt[s_start[s] + j] = ~0ull;
         }
         __syncthreads();
+        GCC_PH_MARK(phc, 4);  // scan + reservations (+ barrier)
 #pragma unroll
         for (int k = 0; k < P1P; ++k)
             if (ok[k]) s_srt[s_start[ua[k] >> kSliceBits] + rk[k]] = ((u64)va[k] << 32) | ua[k];
+        GCC_PH_MARK(phc, 5);  // scatter
         __syncthreads();
+        GCC_PH_MARK(phc, 6);
         const u32 tot4 = (s_start[ns - 1] + pad4(s_cnt[ns - 1])) / 4;
         for (u32 x4 = threadIdx.x; x4 < tot4; x4 += P1B) {
             const u64x2 ea = reinterpret_cast<const u64x2*>(s_srt)[2 * x4];      // slot 4 x4 is never padding
@@ -384,7 +424,9 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
             }
         }
         __syncthreads();
+        GCC_PH_MARK(phc, 7);  // write-out (+ barrier)
     }
+    GCC_PH_FLUSH(phc, 0);
     // the unused tails of this block's chunks: padding entries (P2 skips them)
     for (u32 s = 0; s < ns; ++s)
         for (u32 i = s_cpos[s] + threadIdx.x; i < s_cend[s]; i += P1B) bk_hi[s_base[s] + i] = kPadHi;
@@ -471,6 +513,8 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         runs.cpos[s] = runs.cend[s] = 0;
     }
     if (threadIdx.x == 0) s_slow = 0;
+    [[maybe_unused]] PhaseClock phc;
+    GCC_PH_START(phc);
     // the first seeding level (hub_only): C = {h}, so only h's slice has sources in C: its sample alone, in cps
     // parts (the other 127 of C4's 128 sample buckets would be streamed for nothing)
     const u32 hub_sl = (!FINAL && hub_only) ? (m->gmin >> kSliceBits) : 0u;
@@ -553,6 +597,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         };
         load_round(0);
         for (u32 p0 = 0; p0 < np; p0 += kRoundItems) {
+            GCC_PH_MARK(phc, 7);  // (previous round's write-out / item switch)
             u32* s_cnt = s_cnt2 + rb * kMaxSlicesLds;
             u32 ua[PER], va[PER], rk[PER];
             bool in[PER];
@@ -589,6 +634,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 in[k] = in[k] && va[k] < cap;
             }
             if (bad) flag_err(err, kErrP2);
+            GCC_PH_MARK(phc, 0);  // waited for this round's loads, decoded
             if (p0 + kRoundItems < np) load_round(p0 + kRoundItems);  // next round in flight
             bool emit[PER];
             u32 slow_m = 0;  // FINAL: this lane's slow edges (source not in C), bit k
@@ -599,6 +645,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 if (emit[k]) rk[k] = atomicAdd(&s_cnt[va[k] >> kSliceBits], 1u);
                 slow_m |= (u32)(in[k] && !iu) << k;
             }
+            GCC_PH_MARK(phc, 1);  // source lookups + LDS counting
             if constexpr (FINAL) {  // the slow edges: into this block's region of the slow list, one LDS add per wave
                 const u32 ns_l = (u32)__popc(slow_m);
                 u32 incl = ns_l;
@@ -624,7 +671,9 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                         ring_push((spill_m >> k) & 1u, ua[k], va[k], ring, wq, wd, parent, drain_at, 0xFFFFFFFFu);
                 }
             }
+            GCC_PH_MARK(phc, 2);  // slow-list stores
             __syncthreads();  // (1) counts of this round complete
+            GCC_PH_MARK(phc, 3);
             // runs padded to a multiple of 4 with UNSEEN (P3 skips it): a lane writes 4 targets per store
             count_scan<kP2Block>(s_cnt, s_start, ns, s_wsum);
             for (u32 s = threadIdx.x; s < ns; s += kP2Block) {
@@ -634,10 +683,13 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 s_cnt2[(rb ^ 1) * kMaxSlicesLds + s] = 0;  // the next round's buffer
             }
             __syncthreads();  // (2) starts + reservations
+            GCC_PH_MARK(phc, 4);
 #pragma unroll
             for (int k = 0; k < PER; ++k)
                 if (emit[k]) s_vt[s_start[va[k] >> kSliceBits] + rk[k]] = va[k];
+            GCC_PH_MARK(phc, 5);
             __syncthreads();  // (3) tile in bucket order
+            GCC_PH_MARK(phc, 6);
             const u32 tot4 = (s_start[ns - 1] + pad4(s_cnt[ns - 1])) / 4;
             for (u32 x4 = threadIdx.x; x4 < tot4; x4 += kP2Block) {
                 const u4 v = reinterpret_cast<const u4*>(s_vt)[x4];  // slot 4 x4 is never padding
@@ -661,6 +713,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         }
     }
     __syncthreads();
+    if constexpr (FINAL && !SEG) GCC_PH_FLUSH(phc, 1);
     // the unused tails of this block's chunks: UNSEEN (P3 skips them)
     for (u32 s = 0; s < ns; ++s)
         for (u32 i = runs.cpos[s] + threadIdx.x; i < runs.cend[s]; i += kP2Block) vl.hi[s_vbase[s] + i] = kPadV;

@@ -2428,6 +2428,23 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                      "(%.1f %%), overflow %u, spill %u, g=%u\n", (unsigned long long)n, ns,
                      (unsigned long long)bk_used, (unsigned long long)vl_used, 100.0 * vl_used / n,
                      (unsigned long long)slow, 100.0 * slow / n, hm.ovf_cur, hm.spill, hm.gmin);
+#ifdef GCC_PHASES
+        unsigned long long ph[2][16];
+        HIP_TRY(hipMemcpyFromSymbol(ph, HIP_SYMBOL(bk::gcc_phase_acc), sizeof(ph)));
+        static const char* const names[2][8] = {
+            {"loads", "barrier0", "count", "barrier1", "scan+reserve+barrier2", "scatter", "barrier3", "write-out+barrier4"},
+            {"loads+decode", "lookup+count", "slow stores", "barrier1", "scan+reserve+barrier2", "scatter", "barrier3",
+             "write-out/item"}};
+        for (int k = 0; k < 2; ++k) {
+            unsigned long long tot = 0;
+            for (int j = 0; j < 8; ++j) tot += ph[k][j];
+            std::fprintf(stderr, "[phases] %s:", k ? "P2" : "P1");
+            for (int j = 0; j < 8; ++j) std::fprintf(stderr, " %s %.1f%%", names[k][j], 100.0 * ph[k][j] / (tot ? tot : 1));
+            std::fprintf(stderr, " (total %.3g clk)\n", (double)tot);
+        }
+        unsigned long long zero[2][16] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(bk::gcc_phase_acc), zero, sizeof(zero)));
+#endif
     }
     return GCC_OK;
 }

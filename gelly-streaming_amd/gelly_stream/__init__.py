@@ -11,7 +11,7 @@ All device work goes through libgelly_cc.so (include/gelly_cc.h); there is no CP
 """
 from .aggregation import (EdgeBatch, EdgesFold, Merger, ReduceFunction, SummaryAggregation, SummaryBulkAggregation,
                           SummaryTreeReduce)
-from .bipartite import BipartitenessCheck, Candidates, SignedVertex
+from .bipartite import BipartitenessCheck, Candidates, LiteralBipartitenessCheck, LiteralCandidates, SignedVertex
 from .edgestream import SimpleEdgeStream
 from .library import CombineCC, ConnectedComponents, ConnectedComponentsTree, UpdateCC
 from .longids import IdDictionary, LongDisjointSet
@@ -20,7 +20,8 @@ from .summaries import DisjointSet
 
 __all__ = [
     "BipartitenessCheck", "Candidates", "CombineCC", "ConnectedComponents", "ConnectedComponentsTree", "DisjointSet",
-    "EdgeBatch", "EdgesFold", "GellyCCError", "IdDictionary", "LongDisjointSet", "Merger", "ReduceFunction",
+    "EdgeBatch", "EdgesFold", "GellyCCError", "IdDictionary", "LiteralBipartitenessCheck", "LiteralCandidates",
+    "LongDisjointSet", "Merger", "ReduceFunction",
     "SignedVertex", "SimpleEdgeStream", "SummaryAggregation", "SummaryBulkAggregation", "SummaryTreeReduce", "UNSEEN",
     "UpdateCC", "device_count",
 ]

@@ -30,7 +30,7 @@ tests/test_gpu_bipartite.py); DESIGN.md §7.
 from __future__ import annotations
 
 from collections.abc import Mapping
-from ctypes import byref, c_int, c_void_p
+from ctypes import byref, c_int, c_uint64, c_void_p
 from typing import Iterator, NamedTuple, Optional
 
 import numpy as np
@@ -158,6 +158,120 @@ class Candidates:
             call("gcc_signed_words", self.handle, out.ctypes.data, self.id_capacity)
             self._words = out
         return self._words
+
+
+class LiteralCandidates:
+    """Candidates AS WRITTEN (reference-literal mode, csrc/gelly_literal.hip, gcc_literal_*).
+
+    Candidates.merge (:77-192) skips components with identical vertex sets (:91-95), drops a failed second-level
+    merge (:128-131) and files the input's vertices under min(inputKey, selfKey) without moving the self
+    component (:176-189), so its output can hold overlapping "components" and miss odd cycles. This summary
+    reproduces that output exactly — toString() is the reference's line — for a job that depends on it; the
+    signed forest (Candidates above) is the intended semantics. Every fold / merge runs in the reference's order
+    on one wavefront of the device.
+    """
+
+    def __init__(self, id_capacity: int, device: int = 0, entry_capacity: Optional[int] = None):
+        """``new Candidates(true)`` (:31-34). entry_capacity bounds the entries (default 4 x id_capacity, >= 4096)."""
+        self.id_capacity = int(id_capacity)
+        self.device = int(device)
+        self.entry_capacity = int(entry_capacity or max(4096, 4 * self.id_capacity))
+        h = c_void_p()
+        call("gcc_literal_create", self.device, self.id_capacity, self.entry_capacity, byref(h))
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            call("gcc_literal_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> c_void_p:
+        if not self._h:
+            raise ValueError("LiteralCandidates is closed")
+        return self._h
+
+    def getSuccess(self) -> bool:
+        """:44-46"""
+        ok = c_int()
+        call("gcc_literal_success", self.handle, byref(ok))
+        return bool(ok.value)
+
+    def entries(self) -> np.ndarray:
+        """The TreeMap's entries as u64 (component << 32) | (vertex << 1) | sign, sorted (component, vertex)."""
+        n = c_uint64()
+        call("gcc_literal_entries", self.handle, None, 0, byref(n))
+        out = np.empty(n.value, dtype=np.uint64)
+        if n.value:
+            call("gcc_literal_entries", self.handle, out.ctypes.data, n.value, byref(n))
+        return np.sort(out)
+
+    def getMap(self) -> dict[int, dict[int, SignedVertex]]:
+        """:48-50 — component -> (vertex -> SignedVertex), both in key order."""
+        out: dict[int, dict[int, SignedVertex]] = {}
+        for e in self.entries().tolist():
+            c, v, sg = e >> 32, (e & 0xFFFFFFFF) >> 1, e & 1
+            out.setdefault(c, {})[v] = SignedVertex(v, bool(sg))
+        return out
+
+    def merge(self, other: "LiteralCandidates") -> "LiteralCandidates":
+        """:77-139 — this = this.merge(other), exactly as written; returns self."""
+        call("gcc_literal_merge", self.handle, other.handle)
+        return self
+
+    def fold(self, pairs: np.ndarray) -> None:
+        """updateFunction.foldEdges per edge, in order: this = this.merge(edgeToCandidate(v1, v2))."""
+        a = np.ascontiguousarray(pairs, dtype=np.uint32).reshape(-1)
+        if a.size:
+            call("gcc_literal_fold_host", self.handle, a.ctypes.data, a.size // 2)
+
+    def reset(self) -> None:
+        call("gcc_literal_reset", self.handle)
+
+    def toString(self) -> str:
+        """Flink Tuple2.toString of (success, TreeMap), the reference's output line."""
+        if not self.getSuccess():
+            return "(false,{})"
+        comps = ", ".join(f"{c}={{" + ", ".join(f"{v}={sv}" for v, sv in m.items()) + "}"
+                          for c, m in self.getMap().items())
+        return "(true,{" + comps + "})"
+
+    def __str__(self) -> str:
+        return self.toString()
+
+
+class literalUpdateFunction(EdgesFold[LiteralCandidates]):
+    """BipartitenessCheck.updateFunction (:74-96) over LiteralCandidates."""
+
+    def foldEdges(self, candidates: LiteralCandidates, v1: int, v2: int, edgeVal=None) -> LiteralCandidates:
+        candidates.fold(np.array([[v1, v2]], dtype=np.uint32))
+        return candidates
+
+    def foldEdgeBatch(self, candidates: LiteralCandidates, batch: EdgeBatch) -> LiteralCandidates:
+        candidates.fold(batch.pairs())
+        return candidates
+
+
+class literalCombineFunction(ReduceFunction[LiteralCandidates]):
+    """BipartitenessCheck.combineFunction (:108-131) over LiteralCandidates."""
+
+    def reduce(self, c1: LiteralCandidates, c2: LiteralCandidates) -> LiteralCandidates:
+        return c1.merge(c2)
+
+
+class LiteralBipartitenessCheck(SummaryBulkAggregation[LiteralCandidates, LiteralCandidates]):
+    """BipartitenessCheck with the reference's own Candidates semantics: the generic SummaryBulkAggregation
+    topology (partials per partition, timeWindowAll reduce in order, Merger) over LiteralCandidates."""
+
+    def __init__(self, mergeWindowTime: int, id_capacity: int, device: int = 0, entry_capacity: Optional[int] = None):
+        super().__init__(literalUpdateFunction(), literalCombineFunction(),
+                         lambda: LiteralCandidates(id_capacity, device, entry_capacity), mergeWindowTime, False)
 
 
 class updateFunction(EdgesFold[Candidates]):

@@ -125,6 +125,13 @@ _SIGS = {
     "gcc_signed_merge": (c_int, [c_void_p, c_void_p]),
     "gcc_signed_words": (c_int, [c_void_p, c_void_p, c_uint32]),
     "gcc_signed_success": (c_int, [c_void_p, POINTER(c_int)]),
+    "gcc_literal_create": (c_int, [c_int, c_uint32, c_uint32, POINTER(c_void_p)]),
+    "gcc_literal_destroy": (c_int, [c_void_p]),
+    "gcc_literal_reset": (c_int, [c_void_p]),
+    "gcc_literal_fold_host": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_literal_merge": (c_int, [c_void_p, c_void_p]),
+    "gcc_literal_success": (c_int, [c_void_p, POINTER(c_int)]),
+    "gcc_literal_entries": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
 }
 
 MSG_HEADER_BYTES = 16  # GCC_MSG_HEADER_BYTES

@@ -190,6 +190,26 @@ int gcc_signed_merge(gcc_signed* into, gcc_signed* from);
 int gcc_signed_words(gcc_signed* h, uint32_t* out, uint32_t n); /* canonical words of ids [0, n) */
 int gcc_signed_success(gcc_signed* h, int* success);              /* Candidates.getSuccess (:44-46) */
 
+/* ---- Candidates AS WRITTEN (reference-literal mode; csrc/gelly_literal.hip) ----
+ * The signed forest above implements the intended semantics. Candidates.merge itself is not a partition join: it
+ * skips components with identical vertex sets (Candidates.java:91-95), drops a failed second-level merge
+ * (:128-131) and files the input's vertices under min(inputKey, selfKey) without moving the self component
+ * (:176-189). This summary reproduces that output exactly (the state is the TreeMap itself: entries
+ * (component key << 32) | (vertex << 1) | sign), for a job that depends on it. Sequential by definition: one
+ * wavefront runs each fold / merge in the reference's order. Ids < 2^31 - 1; entry_capacity bounds the entries
+ * (a vertex may sit in several components): GCC_E_OOM past it. */
+typedef struct gcc_literal gcc_literal;
+int gcc_literal_create(int device, uint32_t id_capacity, uint32_t entry_capacity, gcc_literal** out);
+int gcc_literal_destroy(gcc_literal* h);
+int gcc_literal_reset(gcc_literal* h); /* new Candidates(true) (:31-34) */
+/* per edge, in order: this = this.merge(edgeToCandidate(v1, v2)) (BipartitenessCheck.java:54-61, :93-95) */
+int gcc_literal_fold_host(gcc_literal* h, const uint32_t* pairs, uint64_t n_edges);
+/* into = into.merge(from) (combineFunction.reduce :128-130; the Merger's reduce(window, summary)) */
+int gcc_literal_merge(gcc_literal* into, gcc_literal* from);
+int gcc_literal_success(gcc_literal* h, int* success); /* Candidates.getSuccess (:44-46) */
+/* the TreeMap's entries, (key << 32) | (vertex << 1) | sign, in no particular order; out = NULL: the count only */
+int gcc_literal_entries(gcc_literal* h, uint64_t* out, uint64_t cap, uint64_t* n);
+
 /* ---- summary reads (DisjointSet.find :71-85, getMatches :49-51; the emitted summary per window) ---- */
 int gcc_forest_compress(gcc_forest* h); /* async: canonical labels; afterwards gcc_forest_device_ptr = labels */
 int gcc_forest_labels(gcc_forest* h, uint32_t* out, uint32_t n); /* compress + copy n labels to host */

@@ -45,8 +45,8 @@ class PyCandidates:
         comp[vertex] = sign
         return True
 
-    def add_all(self, component, vertices):  # :52-59
-        for v, s in vertices.items():
+    def add_all(self, component, vertices):  # :52-59 (vertices.values(): a TreeMap, so in vertex order)
+        for v, s in sorted(vertices.items()):
             if not self.add(component, v, s):
                 return False
         return True
@@ -83,14 +83,14 @@ class PyCandidates:
     def _merge(inp, cand, in_key, self_key):  # :142-192
         in_comp = inp.map[in_key]
         self_comp = cand.map[self_key]
-        merge_by = [v for v in in_comp if v in self_comp]
+        merge_by = [v for v in sorted(in_comp) if v in self_comp]  # inputComponent.keySet(): TreeMap order
         reversed_ = in_comp[merge_by[0]] != self_comp[merge_by[0]]
         for v in merge_by:
             ok = (in_comp[v] != self_comp[v]) if reversed_ else (in_comp[v] == self_comp[v])
             if not ok:
                 return False
         common = min(in_key, self_key)
-        for v, s in list(in_comp.items()):
+        for v, s in sorted(in_comp.items()):  # inputComponent.values(): TreeMap order (a conflict stops midway)
             if not cand.add(common, v, (not s) if reversed_ else s):
                 return False
         return True
