@@ -1710,9 +1710,11 @@ struct FoldTune {
     u64 bucket_min_ids = (u64)kLdsBitmapMaxWords * 64 + 1;
     // since the first level streams only the hub's slice, the whole of it (C1 = every neighbour of h in the batch)
     // + one level over a quarter of every bucket beat three levels over 15 % (profiles/r2c_sweep_seeding.log:
-    // C4 11.0 -> 10.8 ms, the share equal; round 2's first sweep, r2_sweep_c4_p1.log, predates the hub level)
+    // C4 11.0 -> 10.8 ms, the share equal; round 2's first sweep, r2_sweep_c4_p1.log, predates the hub level).
+    // Round 3 (6-B entries, faster P2): 15 % of every bucket for the second level, C4 10.22 -> 10.04 ms (0.15 / 0.2 /
+    // 0.25 / 0.3: 10.04 / 10.06 / 10.22 / 10.33 ms, profiles/r3h_sweep_seed_sample.log)
     int bucket_levels = 2;
-    double bucket_sample = 0.25;
+    double bucket_sample = 0.15;
     double bucket_hub_sample = 1.0;  // the first level's share of the hub's bucket (C = {h}: one slice)
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
     int bucket_defer = 1;        // N labelled by the fold's closing compress instead of a store per id (bucket_join_kernel)

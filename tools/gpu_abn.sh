@@ -1,7 +1,7 @@
 #!/bin/bash
 # Interleaved A/B/n of library builds on one box (GELLY_CC_LIB; "-" = the in-tree build), two rounds each, bench only.
 # A step that fails ends the session. Usage (GPU box):
-#   bash tools/gpu_abn.sh <tag> "<bench args>" name=lib.so [name=lib.so ...]
+#   bash tools/gpu_abn.sh <tag> "<bench args>" name=lib.so[@k=v,...] [name=lib.so[@k=v,...] ...]
 set -o pipefail
 TAG=$1
 ARGS=$2
@@ -15,9 +15,11 @@ for r in 1 2; do
   for nl in "$@"; do
     name=${nl%%=*}
     lib=${nl#*=}
+    tune=""
+    case $lib in *@*) tune="--tune ${lib#*@}"; lib=${lib%%@*} ;; esac
     echo "== $name round $r"
-    if [ "$lib" = "-" ]; then timeout -k 10 240 $B > "$OUT/${name}_$r.json" 2> "$OUT/${name}_$r.err" || exit $?
-    else GELLY_CC_LIB=$ROOT/$lib timeout -k 10 240 $B > "$OUT/${name}_$r.json" 2> "$OUT/${name}_$r.err" || exit $?; fi
+    if [ "$lib" = "-" ]; then timeout -k 10 240 $B $tune > "$OUT/${name}_$r.json" 2> "$OUT/${name}_$r.err" || exit $?
+    else GELLY_CC_LIB=$ROOT/$lib timeout -k 10 240 $B $tune > "$OUT/${name}_$r.json" 2> "$OUT/${name}_$r.err" || exit $?; fi
   done
 done
 for f in "$OUT"/*_[12].json; do python3 -c "
