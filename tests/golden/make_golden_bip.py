@@ -242,6 +242,13 @@ def main():
     # reference reports success
     stream_fixture("same_vertex_sets_p2", np.array([[1, 2], [2, 3], [1, 3], [3, 2]]), [0, 4], 4, partitions=2,
                    note="Candidates.java:92-95 skips components with identical vertex sets: the triangle is missed")
+    # round 3 (the reference-literal mode's coverage): uniform random graphs, not bipartite in general, over several
+    # windows and partitions: overlapping components, dropped second-level failures and fail() all occur
+    for name, V, E, starts, parts in (("random_gnm_p3", 64, 120, [0, 25, 60, 120], 3),
+                                      ("random_sparse_p2", 400, 300, [0, 100, 200, 300], 2),
+                                      ("random_sparse_p5", 1000, 700, [0, 350, 700], 5)):
+        e5 = rng.integers(0, V, (E, 2))
+        stream_fixture(name, e5, starts, V, partitions=parts)
 
 
 if __name__ == "__main__":

@@ -80,6 +80,9 @@ DIVERGENT = {
     "bip_closes_odd_cycle.json": {0: "partition", 2: "success"},
     "bip_large_bipartite_p4.json": {0: "partition", 1: "partition"},
     "bip_same_vertex_sets_p2.json": {0: "success"},
+    "bip_random_gnm_p3.json": {0: "partition"},
+    "bip_random_sparse_p2.json": {0: "partition"},
+    "bip_random_sparse_p5.json": {0: "partition"},
 }
 
 
