@@ -734,7 +734,10 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
 // changed word): SEED: out = the bitmap of C itself (C grows for the next level; the block's minimum new id goes
 // to m->gmin); FINAL: out = N, the bitmap of the ids reached from C (bucket_hook_kernel hooks them under g, once
 // each). The v-list streams 16 B per lane, kP3Q loads in flight.
-constexpr int kP3Q = 4;
+#ifndef GCC_P3Q
+#define GCC_P3Q 8
+#endif
+constexpr int kP3Q = GCC_P3Q;  // 4-entry groups per thread per iteration: 8 beat 4 and 2 (C4 P3 0.69 / 0.75 / 0.85 ms, profiles/r3p_ab_p3_loads.log)
 template <bool FINAL>
 __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ bits, u32* __restrict__ out,
                                                               u32 nwords32, u32 ns, Meta* __restrict__ m,
