@@ -24,6 +24,15 @@ namespace bk {
 constexpr u32 kSliceBits = 19;                  // ids per slice: 2^19 -> a 64 KiB bitmap slice in LDS
 constexpr u32 kSliceIds = 1u << kSliceBits;
 constexpr u32 kSliceWords = kSliceIds / 32;     // u32 words per slice (16384)
+// v-lists (P2's output, P3's input) are split by TARGET slices of 2^kVSliceBits ids (round 3: 2^20, a 128 KiB bitmap
+// slice in P3's LDS, which holds nothing else): half as many lists as buckets, so P2 keeps half as many write streams
+// open (2 per list: lo, hi), counts and scans half as many runs per round and writes them twice as long
+#ifndef GCC_VSLICE_BITS
+#define GCC_VSLICE_BITS 20
+#endif
+constexpr u32 kVSliceBits = GCC_VSLICE_BITS;
+constexpr u32 kVSliceWords = (1u << kVSliceBits) / 32;
+__host__ __device__ inline u32 vslices(u32 cap) { return (u32)(((u64)cap + (1u << kVSliceBits) - 1) >> kVSliceBits); }
 // P1 geometry (tune.bucket_p1): 0 = 512 threads x 16 edges (8192-edge tiles, 2 blocks per CU), 1 = 1024 x 16
 // (16384-edge tiles, one block per CU: runs twice as long per (tile, bucket))
 constexpr int kP1Block = 512;
@@ -121,8 +130,8 @@ __device__ __forceinline__ bool bk_decode(u32 lo, u16 hi, u32 sbase, u32& u, u32
 }
 
 // ---- v-list entries: 3 bytes (round 3; round 2 stored the u32 target). A v-list belongs to one target slice, so an
-// entry holds the target's 19 slice-local bits: lo (u16) = x[15:0], hi (u8) = x[18:16]; hi = 0xFF marks padding
-// or an unused chunk tail. P2 writes and P3 reads 3 B per listed edge instead of 4.
+// entry holds the target's kVSliceBits slice-local bits: lo (u16) = x[15:0], hi (u8) = x[kVSliceBits-1:16]; hi = 0xFF
+// marks padding or an unused chunk tail. P2 writes and P3 reads 3 B per listed edge instead of 4.
 typedef uint8_t u8;
 constexpr u8 kPadV = 0xFF;
 struct VList {
@@ -228,6 +237,7 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     trace_start(kTrBkLayout);
     __shared__ u32 s_cu[kMaxSlicesLds], s_cv[kMaxSlicesLds];
     __shared__ u64 s_scan[1024];
+    const u32 nvs = vslices(cap);
     for (u32 s = threadIdx.x; s < ns; s += 1024) s_cu[s] = s_cv[s] = 0;
     __syncthreads();
     const u64 n_smp = n < kSample ? n : kSample;
@@ -248,20 +258,20 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
             const u32 u = (u32)e[i], v = (u32)(e[i] >> 32);
             if (u < cap && v < cap) {
                 atomicAdd(&s_cu[u >> kSliceBits], 1u);
-                atomicAdd(&s_cv[v >> kSliceBits], 1u);
+                atomicAdd(&s_cv[v >> kVSliceBits], 1u);
             }
         }
     }
     __syncthreads();
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
         m->bk_cap[s] = est_cap(s_cu[s], n, n_smp, bk_blocks);
-        m->vl_cap[s] = est_cap(s_cv[s], n, n_smp, vl_blocks);
         m->bk_cur[s] = 0;
+        if (s < nvs) m->vl_cap[s] = est_cap(s_cv[s], n, n_smp, vl_blocks);
         m->vl_cur[s] = 0;
     }
     __syncthreads();
     block_prefix(m->bk_cap, m->bk_base, ns, s_scan);
-    block_prefix(m->vl_cap, m->vl_base, ns, s_scan);
+    block_prefix(m->vl_cap, m->vl_base, nvs, s_scan);
     if (threadIdx.x < 16) m->work[threadIdx.x] = 0;
     if (threadIdx.x == 0) m->nseg = 0;
     if (threadIdx.x == 0) m->ring_used = 0;
@@ -438,16 +448,17 @@ __device__ __forceinline__ void item_range(u64 len, u32 part, u32 cps, u64& lo, 
     hi = len * (part + 1) / cps;
 }
 
-// Load slice s of the bitmap (kSliceWords u32) into LDS (16-B loads, 8 in flight per thread).
-template <int BLOCK>
+// Load slice s of the bitmap (WORDS u32: kSliceWords for a bucket, kVSliceWords for a v-list) into LDS (16-B loads,
+// 8 in flight per thread).
+template <int BLOCK, u32 WORDS = kSliceWords>
 __device__ __forceinline__ void load_slice(u32* s_bits, const u32* __restrict__ bits, u32 s, u32 nwords32) {
     typedef u32 u4 __attribute__((ext_vector_type(4)));
-    const u32 w0 = s * kSliceWords;
-    const u32 nw = w0 + kSliceWords <= nwords32 ? kSliceWords : (w0 < nwords32 ? nwords32 - w0 : 0);
-    if (nw == kSliceWords) {
-        lds_fill<BLOCK>(reinterpret_cast<u4*>(s_bits), reinterpret_cast<const u4*>(bits + w0), kSliceWords / 4);
+    const u32 w0 = s * WORDS;
+    const u32 nw = w0 + WORDS <= nwords32 ? WORDS : (w0 < nwords32 ? nwords32 - w0 : 0);
+    if (nw == WORDS) {
+        lds_fill<BLOCK>(reinterpret_cast<u4*>(s_bits), reinterpret_cast<const u4*>(bits + w0), WORDS / 4);
     } else {  // the last, partial slice
-        for (u32 w = threadIdx.x; w < kSliceWords; w += BLOCK) s_bits[w] = w < nw ? bits[w0 + w] : 0u;
+        for (u32 w = threadIdx.x; w < WORDS; w += BLOCK) s_bits[w] = w < nw ? bits[w0 + w] : 0u;
     }
 }
 
@@ -507,7 +518,8 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     for (u32 s = threadIdx.x; s < 2 * kMaxSlicesLds; s += kP2Block) s_cnt2[s] = 0;
     const Runs runs{s_run, s_run + kMaxSlicesLds, s_run + 2 * kMaxSlicesLds, s_run + 3 * kMaxSlicesLds,
                     s_run + 4 * kMaxSlicesLds, s_run + 5 * kMaxSlicesLds};
-    for (u32 s = threadIdx.x; s < ns; s += kP2Block) {  // the v-list layout, once per block
+    const u32 nvs = vslices(cap);  // v-lists: target slices of 2^kVSliceBits ids
+    for (u32 s = threadIdx.x; s < nvs; s += kP2Block) {  // the v-list layout, once per block
         s_vcap[s] = m->vl_cap[s];
         s_vbase[s] = m->vl_base[s];
         runs.cpos[s] = runs.cend[s] = 0;
@@ -642,7 +654,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             for (int k = 0; k < PER; ++k) {
                 const u32 iu = in[k] ? lds_bit(s_bits, ua[k] - sbase) : 0u;
                 emit[k] = in[k] && iu;
-                if (emit[k]) rk[k] = atomicAdd(&s_cnt[va[k] >> kSliceBits], 1u);
+                if (emit[k]) rk[k] = atomicAdd(&s_cnt[va[k] >> kVSliceBits], 1u);
                 slow_m |= (u32)(in[k] && !iu) << k;
             }
             GCC_PH_MARK(phc, 1);  // source lookups + LDS counting
@@ -675,8 +687,8 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             __syncthreads();  // (1) counts of this round complete
             GCC_PH_MARK(phc, 3);
             // runs padded to a multiple of 4 with UNSEEN (P3 skips it): a lane writes 4 targets per store
-            count_scan<kP2Block>(s_cnt, s_start, ns, s_wsum);
-            for (u32 s = threadIdx.x; s < ns; s += kP2Block) {
+            count_scan<kP2Block>(s_cnt, s_start, nvs, s_wsum);
+            for (u32 s = threadIdx.x; s < nvs; s += kP2Block) {
                 const u32 pc = pad4(s_cnt[s]);
                 if (pc) reserve_run(runs, s, pc, &m->vl_cur[s], s_vcap[s]);
                 for (u32 j = s_cnt[s]; j < pc; ++j) s_vt[s_start[s] + j] = 0xFFFFFFFFu;
@@ -686,20 +698,21 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             GCC_PH_MARK(phc, 4);
 #pragma unroll
             for (int k = 0; k < PER; ++k)
-                if (emit[k]) s_vt[s_start[va[k] >> kSliceBits] + rk[k]] = va[k];
+                if (emit[k]) s_vt[s_start[va[k] >> kVSliceBits] + rk[k]] = va[k];
             GCC_PH_MARK(phc, 5);
             __syncthreads();  // (3) tile in bucket order
             GCC_PH_MARK(phc, 6);
-            const u32 tot4 = (s_start[ns - 1] + pad4(s_cnt[ns - 1])) / 4;
+            const u32 tot4 = (s_start[nvs - 1] + pad4(s_cnt[nvs - 1])) / 4;
             for (u32 x4 = threadIdx.x; x4 < tot4; x4 += kP2Block) {
                 const u4 v = reinterpret_cast<const u4*>(s_vt)[x4];  // slot 4 x4 is never padding
-                const u32 s = v.x >> kSliceBits;
+                const u32 s = v.x >> kVSliceBits;
                 const u32 off = run_pos(runs, s, 4 * x4 - s_start[s]);  // a multiple of 4: one chunk
                 if (off != 0xFFFFFFFFu) {  // 8-B lo / 4-B hi stores (bases: 16-entry multiples, off: 4)
                     const u16x4 lo = {(u16)v.x, (u16)v.y, (u16)v.z, (u16)v.w};
-                    const u32 hi = (v.x >> 16 & 7u) | (v.y == 0xFFFFFFFFu ? kPadV : (v.y >> 16 & 7u)) << 8 |
-                                   (v.z == 0xFFFFFFFFu ? kPadV : (v.z >> 16 & 7u)) << 16 |
-                                   (u32)(v.w == 0xFFFFFFFFu ? kPadV : (v.w >> 16 & 7u)) << 24;
+                    constexpr u32 kHm = (1u << (kVSliceBits - 16)) - 1;  // the local id's bits above 16
+                    const u32 hi = (v.x >> 16 & kHm) | (v.y == 0xFFFFFFFFu ? kPadV : (v.y >> 16 & kHm)) << 8 |
+                                   (v.z == 0xFFFFFFFFu ? kPadV : (v.z >> 16 & kHm)) << 16 |
+                                   (u32)(v.w == 0xFFFFFFFFu ? kPadV : (v.w >> 16 & kHm)) << 24;
                     *reinterpret_cast<u16x4*>(vl.lo + s_vbase[s] + off) = lo;
                     *reinterpret_cast<u32*>(vl.hi + s_vbase[s] + off) = hi;
                 } else if (FINAL) {  // the v-list is full: (u in C, v) = union(g, v) now
@@ -715,7 +728,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     __syncthreads();
     if constexpr (FINAL && !SEG) GCC_PH_FLUSH(phc, 1);
     // the unused tails of this block's chunks: UNSEEN (P3 skips them)
-    for (u32 s = 0; s < ns; ++s)
+    for (u32 s = 0; s < nvs; ++s)
         for (u32 i = runs.cpos[s] + threadIdx.x; i < runs.cend[s]; i += kP2Block) vl.hi[s_vbase[s] + i] = kPadV;
     if constexpr (FINAL) {  // the rest of this wave's ring; the block's slow count
         for (; wd < wq; wd += 64) {
@@ -744,15 +757,15 @@ __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ 
                                                               VList vl, u32 cps, u32 work_slot,
                                                               u32 cap, u32* __restrict__ err) {
     trace_start(FINAL ? kTrBkP3 : kTrBkP3Seed);
-    extern __shared__ __attribute__((aligned(16))) u32 s_bits[];  // kSliceWords
+    extern __shared__ __attribute__((aligned(16))) u32 s_bits[];  // kVSliceWords
     __shared__ u32 s_item, s_min;
     u32 cur_slice = 0xFFFFFFFFu;
-    const u32 n_items = ns * cps;
+    const u32 n_items = ns * cps;  // ns: the v-list count (vslices)
     u32 lmin = 0xFFFFFFFFu;
     auto flush_slice = [&]() {  // this block's new members of cur_slice -> out
         if (cur_slice == 0xFFFFFFFFu) return;
-        const u32 w0 = cur_slice * kSliceWords;
-        for (u32 w = threadIdx.x; w < kSliceWords && w0 + w < nwords32; w += kP3Block) {
+        const u32 w0 = cur_slice * kVSliceWords;
+        for (u32 w = threadIdx.x; w < kVSliceWords && w0 + w < nwords32; w += kP3Block) {
             const u32 nw = s_bits[w] & ~bits[w0 + w];
             if (nw && (!FINAL || (nw & ~out[w0 + w]))) atomicOr(&out[w0 + w], nw);
         }
@@ -777,13 +790,13 @@ __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ 
         if (sl != cur_slice) {
             flush_slice();
             __syncthreads();
-            load_slice<kP3Block>(s_bits, bits, sl, nwords32);
+            load_slice<kP3Block, kVSliceWords>(s_bits, bits, sl, nwords32);
             cur_slice = sl;
             __syncthreads();
         }
         const u64* vlo = reinterpret_cast<const u64*>(vl.lo + m->vl_base[sl]);  // 4 entries per 8 B (aligned)
         const u32* vhi = reinterpret_cast<const u32*>(vl.hi + m->vl_base[sl]);  // 4 entries per 4 B
-        const u32 sbase = sl << kSliceBits;
+        const u32 sbase = sl << kVSliceBits;
         const u64 qlo = lo / 4, qhi = (hi + 3) / 4;  // 4-entry groups; entries outside [lo, hi) masked
         for (u64 b = qlo; b < qhi; b += (u64)kP3Q * kP3Block) {
             u64 rl[kP3Q];

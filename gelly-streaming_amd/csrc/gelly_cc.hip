@@ -2324,7 +2324,14 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     // P2 block at most)
     const u32 cps_hub = (u32)std::max<u64>(1, std::min<u64>(p2_blocks, (u64)((double)n * t.bucket_hub_sample) / ns / 16384));
     const u32 frac_hub = (u32)std::max(0.0, std::min(65536.0, t.bucket_hub_sample * 65536.0));
-    const size_t f_lds = slice_filter_lds(), h_lds = bk::kSliceWords * sizeof(u32);
+    const size_t f_lds = slice_filter_lds(), h_lds = bk::kVSliceWords * sizeof(u32);
+    // P3's items: parts of the v-lists (target slices of 2^kVSliceBits ids, fewer than the buckets). Each item loads
+    // its list's bitmap slice into LDS: as many parts per list as the buckets have per slice would load twice the
+    // bytes of slices, so a v-list has (slice size ratio) times fewer parts
+    const u32 nvs = bk::vslices(h->cap);
+    const u32 vratio = 1u << (bk::kVSliceBits - bk::kSliceBits);
+    const u32 cps_v = std::max<u32>(1, cps * ns / nvs / vratio);
+    const u32 cps_seed_v = std::max<u32>(1, cps_seed * ns / nvs / vratio);
     const size_t vl_cur_off = offsetof(bk::Meta, vl_cur);
     u32 slot = 0;
     rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta,
@@ -2355,7 +2362,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                       (bk::SlowSeg*)nullptr);
         if (!rc)
             rc = launch_k(h, "seed_hook", 0, bk::slice_hook_kernel<false>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                          bits, nw32, ns, h->d_meta, vl, cps_seed, slot++, h->cap, h->d_err);
+                          bits, nw32, nvs, h->d_meta, vl, cps_seed_v, slot++, h->cap, h->d_err);
     }
     // parent[] := C ? g : UNSEEN (the reset), then every bucketed edge, the overflow list, a spill
     if (!rc)
@@ -2372,7 +2379,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
 #undef GCC_P2_FINAL
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                      h->d_nbits, nw32, ns, h->d_meta, vl, cps, slot++, h->cap, h->d_err);
+                      h->d_nbits, nw32, nvs, h->d_meta, vl, cps_v, slot++, h->cap, h->d_err);
     const bool defer = t.bucket_defer != 0;
     if (!rc)
         rc = defer ? launch_k(h, "bucket_join", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
@@ -2394,7 +2401,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                       (const u32*)giant, reinterpret_cast<u64*>(h->d_bk), slow_cap2, h->cap, h->d_err, h->d_seg);
         if (!rc)
             rc = launch_k(h, "slice_hook2", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                          h->d_nbits, nw32, ns, h->d_meta, vl, cps, slot++, h->cap, h->d_err);
+                          h->d_nbits, nw32, nvs, h->d_meta, vl, cps_v, slot++, h->cap, h->d_err);
         if (!rc)
             rc = defer ? launch_k(h, "bucket_join2", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock),
                                   0, h->d_parent, bits, (const u32*)h->d_nbits, nw32, (const u32*)giant,
@@ -2772,8 +2779,8 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::slice_filter_kernel<true>, (int)slice_filter_lds()},
         {(const void*)bk::slice_filter_kernel<true, true>, (int)slice_filter_lds()},
         {(const void*)bk::slice_filter_kernel<true, false, 12>, (int)slice_filter_lds(12)},
-        {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kSliceWords * sizeof(u32))},
-        {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kSliceWords * sizeof(u32))},
+        {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kVSliceWords * sizeof(u32))},
+        {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kVSliceWords * sizeof(u32))},
         {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
         {(const void*)bk::bucket_kernel<512, 16>, (int)bk::p1_lds(512, 16)},
         {(const void*)bk::bucket_kernel<1024, 16>, (int)bk::p1_lds(1024, 16)},
