@@ -1,5 +1,5 @@
 #!/bin/bash
-# Benches of every BASELINE config at HEAD (one box) + a C4 seeding-sample sweep. A step that fails ends the session.
+# Benches of every BASELINE config at HEAD (one box) [+ a C4 seeding-sample sweep with SWEEP=1]. A step that fails ends the session.
 # Usage (GPU box): bash tools/gpu_configs.sh <tag>
 set -o pipefail
 TAG=${1:-r3}
@@ -14,9 +14,11 @@ run() {  # name, bench args...
   timeout -k 10 240 $B "$@" > "$OUT/$name.json" 2> "$OUT/$name.err"
 }
 run c4 || exit $?
-run c4_s15 --tune bucket_sample=0.15 || exit $?
-run c4_s20 --tune bucket_sample=0.2 || exit $?
-run c4_s30 --tune bucket_sample=0.3 || exit $?
+if [ "${SWEEP:-0}" = 1 ]; then  # the seeding-sample sweep (SWEEP=1)
+  run c4_s10 --tune bucket_sample=0.1 || exit $?
+  run c4_s20 --tune bucket_sample=0.2 || exit $?
+  run c4_s30 --tune bucket_sample=0.3 || exit $?
+fi
 run c4share --workload c4_share || exit $?
 run c5 --workload c5_adversarial || exit $?
 run c2w16 --workload c2_rmat20 --window-edges 1048576 || exit $?
