@@ -40,21 +40,26 @@ constexpr int kP1Per = 16;                      // edges per thread per tile
 constexpr u32 kP1Tile = kP1Block * kP1Per;      // the smallest tile (bucket_applies: a batch of >= 2 tiles)
 constexpr int kP2Block = 1024;
 // P2 entries per thread per round (tune bucket_p2_per: 8 or 12): a round of kP2Block * PER entries, and at most that
-// many v's in the round's LDS tile + up to 3 padding slots per slice (kMaxSlicesLds)
+// many v's in the round's LDS tile + up to 3 padding slots per v-list (kMaxVLists)
 constexpr u32 p2_round(int per) { return (u32)kP2Block * per; }
-constexpr u32 p2_tile(int per) { return p2_round(per) + 3 * 256; }
-constexpr u32 kMaxSlicesLds = 256;              // LDS per-slice state: id ranges up to 2^27 (larger: the old path)
+constexpr u32 p2_tile(int per) { return p2_round(per) + 3 * 256; }  // (3 x kMaxVLists)
+// id ranges up to 2^28 (larger: the unbucketed fold): at most 512 buckets (2^19-id source slices) and 256 v-lists
+// (2^20-id target slices). P1's per-bucket LDS state is sized per instantiation (P1 MAXB: 256 up to 2^27 ids, 512
+// beyond, with a smaller tile); P2 / P3 keep per-v-list state only
+constexpr u32 kMaxBuckets = 512;
+constexpr u32 kMaxVLists = 256;
+static_assert(((u64)kMaxBuckets << kSliceBits) == ((u64)kMaxVLists << kVSliceBits), "the same id range");
 constexpr int kP3Block = 1024;
 constexpr u32 kMaxP2Blocks = 1024;
 
-// Per-forest metadata (device), kMaxSlicesLds entries each where per slice.
+// Per-forest metadata (device): per bucket (kMaxBuckets) and per v-list (kMaxVLists).
 struct Meta {
-    u64 bk_base[kMaxSlicesLds];  // bucket s: edges [bk_base[s], bk_base[s] + bk_cap[s]) of the bucket storage
-    u32 bk_cap[kMaxSlicesLds];
-    u32 bk_cur[kMaxSlicesLds];   // reservation cursor (may pass bk_cap: the rest went to the overflow list)
-    u64 vl_base[kMaxSlicesLds];  // v-list s (targets in slice s): entries [vl_base[s], vl_base[s] + vl_cap[s])
-    u32 vl_cap[kMaxSlicesLds];
-    u32 vl_cur[kMaxSlicesLds];   // may pass vl_cap: those v's were hooked inline (FINAL) or dropped (SEED)
+    u64 bk_base[kMaxBuckets];  // bucket s: edges [bk_base[s], bk_base[s] + bk_cap[s]) of the bucket storage
+    u32 bk_cap[kMaxBuckets];
+    u32 bk_cur[kMaxBuckets];   // reservation cursor (may pass bk_cap: the rest went to the overflow list)
+    u64 vl_base[kMaxVLists];   // v-list s (targets in slice s): entries [vl_base[s], vl_base[s] + vl_cap[s])
+    u32 vl_cap[kMaxVLists];
+    u32 vl_cur[kMaxVLists];    // may pass vl_cap: those v's were hooked inline (FINAL) or dropped (SEED)
     u32 work[16];                // per-launch dequeue counters
     u32 ovf_cur;                 // overflow list cursor (may pass its capacity: then `spill`)
     u32 spill;                   // 1: some edge fit neither its bucket nor the overflow list
@@ -106,11 +111,11 @@ typedef uint16_t u16;
 typedef u16 u16x4 __attribute__((ext_vector_type(4)));
 
 // ---- bucket entries: 6 bytes (round 3; round 2 stored the u64 edge). The bucket (= source slice s) already names
-// the source's high bits, so an entry holds the target v (< 2^27: ns <= 256 slices of 2^19 ids) and the source's
-// 19 slice-local bits ul, in two parallel arrays of the same index: lo (u32) = v | ul[4:0] << 27, hi (u16) =
-// ul[18:5]. hi = 0xFFFF (ul never reaches 2^19) marks a padding slot or an unused chunk tail. P1 writes and P2 reads
-// 6 B per edge instead of 8: 25 % of both passes' bucket traffic.
-constexpr u32 kTgtBits = 27;
+// the source's high bits, so an entry holds the target v (< 2^28: ns <= 512 slices of 2^19 ids) and the source's
+// 19 slice-local bits ul, in two parallel arrays of the same index: lo (u32) = v | ul[3:0] << 28, hi (u16) =
+// ul[18:4] (15 bits). hi = 0xFFFF (never 15 bits) marks a padding slot or an unused chunk tail. P1 writes and P2
+// reads 6 B per edge instead of 8: 25 % of both passes' bucket traffic.
+constexpr u32 kTgtBits = 28;
 constexpr u32 kTgtMask = (1u << kTgtBits) - 1;
 constexpr u16 kPadHi = 0xFFFF;
 
@@ -235,10 +240,13 @@ __device__ __forceinline__ void block_prefix(const u32* cap, u64* base, u32 ns, 
 __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                               Meta* __restrict__ m, u32 bk_blocks, u32 vl_blocks) {
     trace_start(kTrBkLayout);
-    __shared__ u32 s_cu[kMaxSlicesLds], s_cv[kMaxSlicesLds];
+    __shared__ u32 s_cu[kMaxBuckets], s_cv[kMaxVLists];
     __shared__ u64 s_scan[1024];
     const u32 nvs = vslices(cap);
-    for (u32 s = threadIdx.x; s < ns; s += 1024) s_cu[s] = s_cv[s] = 0;
+    for (u32 s = threadIdx.x; s < ns; s += 1024) {
+        s_cu[s] = 0;
+        if (s < nvs) s_cv[s] = 0;
+    }
     __syncthreads();
     const u64 n_smp = n < kSample ? n : kSample;
     // the sample: kSample / 1024 = 64 runs of 1024 CONSECUTIVE edges spread evenly over the batch (coalesced, 64
@@ -266,8 +274,10 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
         m->bk_cap[s] = est_cap(s_cu[s], n, n_smp, bk_blocks);
         m->bk_cur[s] = 0;
-        if (s < nvs) m->vl_cap[s] = est_cap(s_cv[s], n, n_smp, vl_blocks);
-        m->vl_cur[s] = 0;
+        if (s < nvs) {
+            m->vl_cap[s] = est_cap(s_cv[s], n, n_smp, vl_blocks);
+            m->vl_cur[s] = 0;
+        }
     }
     __syncthreads();
     block_prefix(m->bk_cap, m->bk_base, ns, s_scan);
@@ -282,7 +292,7 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
 }
 
 // Block-wide exclusive scan of the counts cnt[0..ns), each rounded up to a multiple of 4 (pad4: the runs' padded
-// lengths), into start[] (BLOCK threads, ns <= kMaxSlicesLds). One barrier inside.
+// lengths), into start[] (BLOCK threads, ns <= kMaxBuckets). One barrier inside.
 __device__ __forceinline__ u32 pad4(u32 c) { return (c + 3) & ~3u; }
 template <int BLOCK>
 __device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u32* s_wsum) {
@@ -320,21 +330,21 @@ __device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u
 // P1's dynamic LDS: the tile in bucket order, every bucket's run padded to a multiple of 4 — up to three slots per
 // slice beyond the tile. (Round 2 first sized it to the tile alone: a full tile's last padded slots fell past the
 // allocation and relied on the LDS allocation's rounding slack; a 1024 x 8 geometry with less slack lost edges.)
-constexpr size_t p1_lds(int block, int per) { return ((size_t)block * per + 3 * kMaxSlicesLds) * sizeof(u64); }
+constexpr size_t p1_lds(int block, int per, u32 maxb = 256) { return ((size_t)block * per + 3 * maxb) * sizeof(u64); }
 
-template <int P1B, int P1P>
+template <int P1B, int P1P, u32 MAXB = 256>
 __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                           Meta* __restrict__ m, u32* __restrict__ bk_lo,
                                                           u16* __restrict__ bk_hi, u64* __restrict__ ovf, u32 ovf_cap,
                                                           u32* __restrict__ err) {
     trace_start(kTrBkP1);
-    // the tile in bucket order: dynamic LDS (p1_lds: P1B * P1P + kMaxSlicesLds u64, 66 / 130 KiB), set up like every
-    // kernel's LDS beyond 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-slice state below is static
+    // the tile in bucket order: dynamic LDS (p1_lds: P1B * P1P + 3 MAXB u64, 66 / 130 KiB), set up like every
+    // kernel's LDS beyond 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-bucket state below is static (MAXB >= ns)
+    static_assert(MAXB <= kMaxBuckets, "Meta holds kMaxBuckets buckets");
     extern __shared__ __attribute__((aligned(16))) u64 s_srt[];
-    __shared__ u32 s_cnt[kMaxSlicesLds], s_start[kMaxSlicesLds], s_cap[kMaxSlicesLds];
-    __shared__ u32 s_cpos[kMaxSlicesLds], s_cend[kMaxSlicesLds], s_p1[kMaxSlicesLds], s_l1[kMaxSlicesLds],
-        s_p2[kMaxSlicesLds], s_l2[kMaxSlicesLds];
-    __shared__ u64 s_base[kMaxSlicesLds];
+    __shared__ u32 s_cnt[MAXB], s_start[MAXB], s_cap[MAXB];
+    __shared__ u32 s_cpos[MAXB], s_cend[MAXB], s_p1[MAXB], s_l1[MAXB], s_p2[MAXB], s_l2[MAXB];
+    __shared__ u64 s_base[MAXB];
     __shared__ u32 s_wsum[P1B / 64];
     const Runs runs{s_cpos, s_cend, s_p1, s_l1, s_p2, s_l2};
     typedef u32 u4 __attribute__((ext_vector_type(4)));
@@ -499,13 +509,14 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     u32* s_bits = s_dyn;                                   // kSliceWords
     u32* s_vt = s_dyn + kSliceWords;                       // p2_tile(PER): the round's targets + run padding
-    u32* s_cnt2 = s_vt + p2_tile(PER);                          // 2 x kMaxSlicesLds (double-buffered)
-    u32* s_pc = s_cnt2 + 2 * kMaxSlicesLds;                // kMaxSlicesLds: counts padded to 4
-    u32* s_start = s_pc + kMaxSlicesLds;                   // kMaxSlicesLds
-    u32* s_vcap = s_start + kMaxSlicesLds;                 // kMaxSlicesLds
-    u32* s_run = s_vcap + kMaxSlicesLds;                   // 6 x kMaxSlicesLds: the chunk state (Runs)
-    u64* s_vbase = reinterpret_cast<u64*>(s_run + 6 * kMaxSlicesLds);   // kMaxSlicesLds
-    u64* ring = s_vbase + kMaxSlicesLds + (threadIdx.x >> 6) * kRing;  // FINAL only
+    // per v-list state, kMaxVLists entries each
+    u32* s_cnt2 = s_vt + p2_tile(PER);                     // 2 x (double-buffered counts)
+    u32* s_pc = s_cnt2 + 2 * kMaxVLists;                   // counts padded to 4
+    u32* s_start = s_pc + kMaxVLists;
+    u32* s_vcap = s_start + kMaxVLists;
+    u32* s_run = s_vcap + kMaxVLists;                      // 6 x: the chunk state (Runs)
+    u64* s_vbase = reinterpret_cast<u64*>(s_run + 6 * kMaxVLists);
+    u64* ring = s_vbase + kMaxVLists + (threadIdx.x >> 6) * kRing;  // FINAL only
     __shared__ u32 s_item, s_wsum[kP2Block / 64], s_slow;
     typedef u32 u4 __attribute__((ext_vector_type(4)));
     constexpr int kQ = PER / 2;
@@ -515,9 +526,9 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     u32 wq = 0, wd = 0;  // this wave's ring cursors (FINAL)
     u32 cur_slice = 0xFFFFFFFFu;
     u32 rb = 0;  // round parity: the counter buffer in use
-    for (u32 s = threadIdx.x; s < 2 * kMaxSlicesLds; s += kP2Block) s_cnt2[s] = 0;
-    const Runs runs{s_run, s_run + kMaxSlicesLds, s_run + 2 * kMaxSlicesLds, s_run + 3 * kMaxSlicesLds,
-                    s_run + 4 * kMaxSlicesLds, s_run + 5 * kMaxSlicesLds};
+    for (u32 s = threadIdx.x; s < 2 * kMaxVLists; s += kP2Block) s_cnt2[s] = 0;
+    const Runs runs{s_run, s_run + kMaxVLists, s_run + 2 * kMaxVLists, s_run + 3 * kMaxVLists,
+                    s_run + 4 * kMaxVLists, s_run + 5 * kMaxVLists};
     const u32 nvs = vslices(cap);  // v-lists: target slices of 2^kVSliceBits ids
     for (u32 s = threadIdx.x; s < nvs; s += kP2Block) {  // the v-list layout, once per block
         s_vcap[s] = m->vl_cap[s];
@@ -610,7 +621,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         load_round(0);
         for (u32 p0 = 0; p0 < np; p0 += kRoundItems) {
             GCC_PH_MARK(phc, 7);  // (previous round's write-out / item switch)
-            u32* s_cnt = s_cnt2 + rb * kMaxSlicesLds;
+            u32* s_cnt = s_cnt2 + rb * kMaxVLists;
             u32 ua[PER], va[PER], rk[PER];
             bool in[PER];
             if constexpr (SEG) {
@@ -692,7 +703,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                 const u32 pc = pad4(s_cnt[s]);
                 if (pc) reserve_run(runs, s, pc, &m->vl_cur[s], s_vcap[s]);
                 for (u32 j = s_cnt[s]; j < pc; ++j) s_vt[s_start[s] + j] = 0xFFFFFFFFu;
-                s_cnt2[(rb ^ 1) * kMaxSlicesLds + s] = 0;  // the next round's buffer
+                s_cnt2[(rb ^ 1) * kMaxVLists + s] = 0;  // the next round's buffer
             }
             __syncthreads();  // (2) starts + reservations
             GCC_PH_MARK(phc, 4);

@@ -1564,7 +1564,7 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
 #include "bucket_fold.h"
 
 static constexpr size_t slice_filter_lds(int per = 8) {  // bucket_fold.h slice_filter_kernel's dynamic LDS
-    return (bk::kSliceWords + bk::p2_tile(per) + 11 * bk::kMaxSlicesLds) * sizeof(u32) + bk::kMaxSlicesLds * sizeof(u64) +
+    return (bk::kSliceWords + bk::p2_tile(per) + 11 * bk::kMaxVLists) * sizeof(u32) + bk::kMaxVLists * sizeof(u64) +
            (bk::kP2Block / 64) * kRing * sizeof(u64);
 }
 
@@ -2241,7 +2241,7 @@ static bool bucket_applies(const gcc_forest* h, const u32* d_pairs, u64 n) {
     const FoldTune& t = h->tune;
     return t.bucket && h->pending_reset && h->filter_enabled() && (u64)h->cap >= t.bucket_min_ids &&
            n >= std::max<u64>(t.bucket_min_batch, 2 * bk::kP1Tile) && n < (1ull << 31) &&
-           bucket_slices(h) <= bk::kMaxSlicesLds &&
+           bucket_slices(h) <= bk::kMaxBuckets &&
            ((reinterpret_cast<uintptr_t>(d_pairs) | reinterpret_cast<uintptr_t>(h->d_parent) |
              reinterpret_cast<uintptr_t>(h->d_spare)) & 15) == 0;
 }
@@ -2337,7 +2337,11 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta,
                   p1_blocks, p2_blocks);
     if (!rc)
-        rc = t.bucket_p1 == 1
+        rc = ns > 256  // beyond 2^27 ids: 512 buckets' state and the 16K-edge tile exceed the LDS; 12K-edge tiles
+                 ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 12, 512>, dim3(h->n_cu), dim3(1024),
+                            bk::p1_lds(1024, 12, 512), edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap,
+                            h->d_err)
+             : t.bucket_p1 == 1
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16>, dim3(h->n_cu), dim3(1024), bk::p1_lds(1024, 16),
                             edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err)
              : t.bucket_p1 == 2
@@ -2354,7 +2358,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u64 sample_edges = (u64)((double)n * frac / 65536.0);
     const int levels = std::max(0, std::min(6, t.bucket_levels));
     for (int l = 0; l < levels && !rc; ++l) {
-        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
+        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, nvs * sizeof(u32), h->stream));
         rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
                       f_lds, h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,
                       (const u32*)bits, nw32, ns, h->d_meta, vl, l == 0 ? cps_hub : cps_seed, l == 0 ? frac_hub : frac, slot++, h->tune.drain_at, (u32)(l == 0),
@@ -2369,7 +2373,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         rc = launch_k(h, "bucket_init", 0, bk::bucket_init_kernel, dim3(grid_for(((u64)h->cap + 3) / 4, kMaxGrid)),
                       dim3(kBlock), 0, h->d_parent, h->cap, (const u32*)bits, (const bk::Meta*)h->d_meta, giant);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
+    HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, nvs * sizeof(u32), h->stream));
 #define GCC_P2_FINAL(PER)                                                                                          \
     launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true, false, PER>, dim3(p2_blocks), dim3(bk::kP2Block),    \
              slice_filter_lds(PER), h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,       \
@@ -2394,7 +2398,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (slow2 && !rc) {
         // the bucket storage (consumed by FINAL P2) as u64 slow entries
         const u32 slow_cap2 = (u32)std::min<u64>(0x7FFFFFFEull, h->bk_cap_bytes / 8 / p2_blocks) & ~1u;
-        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, ns * sizeof(u32), h->stream));
+        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, nvs * sizeof(u32), h->stream));
         rc = launch_k(h, "slice_filter2", 0, bk::slice_filter_kernel<true, true>, dim3(p2_blocks), dim3(bk::kP2Block),
                       f_lds, h->d_parent, (const u32*)nullptr, (const bk::u16*)nullptr, (const u64*)h->d_slow,
                       (const u32*)bits, nw32, ns, h->d_meta, vl, 1u, 65536u, slot++, h->tune.drain_at, 0u,
@@ -2785,6 +2789,7 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::bucket_kernel<512, 16>, (int)bk::p1_lds(512, 16)},
         {(const void*)bk::bucket_kernel<1024, 16>, (int)bk::p1_lds(1024, 16)},
         {(const void*)bk::bucket_kernel<1024, 12>, (int)bk::p1_lds(1024, 12)},
+        {(const void*)bk::bucket_kernel<1024, 12, 512>, (int)bk::p1_lds(1024, 12, 512)},
     };
     for (const auto& t : tab) HIP_TRY(hipFuncSetAttribute(t.f, hipFuncAttributeMaxDynamicSharedMemorySize, t.bytes));
     return set_trace_slot();

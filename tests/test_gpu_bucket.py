@@ -127,6 +127,30 @@ def test_bucketed_fold_overflow_and_spill(torch_cuda, hot_share):
         assert mismatch(ds.labels(), oracle_labels(pairs, V)) is None
 
 
+@pytest.mark.parametrize("V", [(1 << 27) + (1 << 20), 1 << 28])
+def test_bucketed_fold_beyond_2_27_ids(torch_cuda, V):
+    """Id ranges past 2^27 (they took the unbucketed fold): 258 / 512 buckets of 2^19 ids, P1's
+    512-bucket instantiation, 28-bit targets in the 6-B entries. A giant (4096 hubs joined to each other and to 2M
+    random ids) plus 2M random pairs over the whole range (the slow / union path), ids up to V - 1."""
+    rng = np.random.default_rng(V & 0xFFFF)
+    hubs = rng.choice(V, size=4096, replace=False).astype(np.uint32)
+    n_h = 1 << 16
+    hub_hub = np.stack([hubs[rng.integers(0, 4096, n_h)], hubs[rng.integers(0, 4096, n_h)]], axis=1)
+    n_s = (1 << 21) - n_h
+    star = np.stack([hubs[rng.integers(0, 4096, n_s)], rng.integers(0, V, n_s, dtype=np.uint32)], axis=1)
+    rand = rng.integers(0, V, size=(1 << 21, 2), dtype=np.uint32)
+    pairs = np.concatenate([hub_hub, star, rand])[rng.permutation(1 << 22)]
+    pairs[-1] = [V - 1, hubs[0]]
+    d = to_device(torch_cuda, pairs)
+    with DisjointSet(V) as ds:
+        ds.tune(**FORCE)
+        ds.enable_timing(1)
+        ds.fold_device(d.data_ptr(), len(pairs))
+        names = [k for k, _, _ in ds.fold_profile()]
+        assert "bucket" in names and "slice_filter" in names, names  # the bucketed path ran
+        assert mismatch(ds.labels(), oracle_labels(pairs, V)) is None
+
+
 @pytest.mark.parametrize("bucketed", [False, True])
 def test_device_batch_id_validation(torch_cuda, bucketed):
     """An edge with an id >= id_capacity in a DEVICE batch is skipped (never dereferenced) and reported once by
