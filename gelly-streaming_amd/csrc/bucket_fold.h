@@ -134,6 +134,13 @@ __device__ __forceinline__ bool bk_decode(u32 lo, u16 hi, u32 sbase, u32& u, u32
     return hi != kPadHi;
 }
 
+// Bucket bases 2 MiB-aligned (the lo array; hi 1 MiB) for batches of >= 2^26 edges: every capacity is rounded up
+// to 2^19 entries. The lists' write frontiers advance in step, and their relative placement matters (a hashed
+// stagger of the bases cost P2 +0.8 ms, profiles/r3af_ab_stagger.log); aligned buckets: C4 9.64 -> 9.52 ms on two
+// boxes (P1 and P2 -0.05 ms each; aligning the v-lists as well: no further change; profiles/r3ag_*, r3ah_*)
+constexpr u64 kBkAlign = 1ull << 19;  // entries
+__host__ __device__ inline bool bk_aligned(u64 n) { return n >= (1ull << 26); }
+
 // ---- v-list entries: 3 bytes (round 3; round 2 stored the u32 target). A v-list belongs to one target slice, so an
 // entry holds the target's kVSliceBits slice-local bits: lo (u16) = x[15:0], hi (u8) = x[kVSliceBits-1:16]; hi = 0xFF
 // marks padding or an unused chunk tail. P2 writes and P3 reads 3 B per listed edge instead of 4.
@@ -146,8 +153,8 @@ struct VList {
 __host__ __device__ inline u64 vl_entries(u64 storage) { return (storage + 15) / 16 * 16; }
 __host__ __device__ inline u64 vl_bytes(u64 storage) { return 3 * vl_entries(storage); }
 
-// the bucket storage of S entries (S a multiple of 16): lo at the start, hi right after (16-B aligned)
-__host__ __device__ inline u64 bk_entries(u64 storage) { return (storage + 15) / 16 * 16; }
+// the bucket storage of S entries (S a multiple of 2^19): lo at the start, hi right after (1 MiB-aligned)
+__host__ __device__ inline u64 bk_entries(u64 storage) { return (storage + kBkAlign - 1) / kBkAlign * kBkAlign; }
 __host__ __device__ inline u64 bk_bytes(u64 storage) { return 6 * bk_entries(storage); }
 
 // Internal consistency checks: every id a kernel takes from an internal list (buckets, slow and overflow lists) and
@@ -171,8 +178,10 @@ constexpr u32 kSlack = 1u << 12;
 #endif
 constexpr u32 kChunk = GCC_KCHUNK;
 
+
 __host__ __device__ inline u64 storage_edges(u64 n, u32 ns, u32 blocks) {
-    return n + n / 4 + (u64)ns * (kSlack + 64 + (u64)blocks * kChunk) + 64;
+    return n + n / 4 + (u64)ns * (kSlack + 64 + (u64)blocks * kChunk) + 64 +
+           (bk_aligned(n) ? (u64)ns * kBkAlign : 0);
 }
 
 __device__ __forceinline__ u32 est_cap(u32 hits, u64 n, u64 n_smp, u32 blocks) {
@@ -273,6 +282,7 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     __syncthreads();
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
         m->bk_cap[s] = est_cap(s_cu[s], n, n_smp, bk_blocks);
+        if (bk_aligned(n)) m->bk_cap[s] = (u32)((m->bk_cap[s] + kBkAlign - 1) / kBkAlign * kBkAlign);
         m->bk_cur[s] = 0;
         if (s < nvs) {
             m->vl_cap[s] = est_cap(s_cv[s], n, n_smp, vl_blocks);

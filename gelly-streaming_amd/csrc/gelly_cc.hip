@@ -1691,7 +1691,12 @@ struct FoldTune {
     // incremental compress (compress_inc_kernel): plain folds record their mutations in a bloom filter when the
     // forest spans >= inc_min_ids ids and a batch is at most 1/inc_div of them (a short window of a big forest)
     bool refresh_labels = false;  // mid-fold refreshes: bitmap only (false) or a full compress (true)
-    bool incremental = true;
+    // OFF by default (end of round 3): with it on, C3 in 1M-edge windows at the defaults ended its last window with
+    // the right seen / component counts and a wrong label digest (a label left at a hooked root) in one full GPU
+    // run (profiles/r3ai_gpu_tests_c3_w1M_stale_label.log), the symptom of round 2's unexplained failure. Until its
+    // mechanism is found every emission takes the full compress; tune incremental=1 opts in (its tests run with
+    // inc_check, which re-derives every incremental compress)
+    bool incremental = false;
     bool inc_inplace = true;  // the incremental compress rewrites only changed parent[] slots (no spare buffer)
     u64 inc_min_ids = 1ull << 22;
     // chosen by speed (round 3, tools/sweep_inc_div.py, profiles/r3c_sweep_inc_div.log): on C3 and C5 the recording
@@ -2292,7 +2297,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     }
     const u32 p1_blocks = 2 * (u32)h->n_cu;  // (bucket_p1 = 1 runs n_cu blocks: fewer writers, same slack bound)
     const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
-    const u64 bk_S = bk::bk_entries(bk::storage_edges(n, ns, p1_blocks));  // entries (a multiple of 16)
+    const u64 bk_S = bk::bk_entries(bk::storage_edges(n, ns, p1_blocks));  // entries (a multiple of 2^19)
     if ((rc = grow(h->d_bk, h->bk_cap_bytes, bk::bk_bytes(bk_S), h->stream))) return rc;
     u32* bk_lo = reinterpret_cast<u32*>(h->d_bk);
     bk::u16* bk_hi = reinterpret_cast<bk::u16*>(h->d_bk + 4 * bk_S);

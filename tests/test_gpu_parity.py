@@ -256,8 +256,9 @@ def test_incremental_compress_windows(torch_cuda):
     want = orc.cc_stream(G.generate_host(cfg), starts, V, partitions=2, threads=2)
     d = device_stream(torch_cuda, cfg)
     inc, full, spare = DisjointSet(V), DisjointSet(V), DisjointSet(V)
+    inc.tune(incremental=1)  # opt-in since the end of round 3
     full.tune(incremental=0)
-    spare.tune(inc_inplace=0)
+    spare.tune(incremental=1, inc_inplace=0)
     side = DisjointSet(V)  # a partial forest merged into `inc` mid-stream (CombineCC)
     side.fold_device(d.data_ptr(), W)
     for w in range(len(starts) - 1):
@@ -537,9 +538,9 @@ KNOB_CASES = {
     "depth": {"depth": 8}, "hook": {"hook": 0}, "drain_at": {"drain_at": 1}, "seed": {"seed": 0},
     "seed_nt": {"seed_nt": 0}, "seed_global": {"seed_global": 1}, "seed_fuse": {"seed_fuse": 0},
     "seed_passes": {"seed_passes": 3}, "seed_div": {"seed_div": 2}, "seed_div1": {"seed_div1": 5},
-    "seed_refresh": {"seed_refresh": 0.5}, "incremental": {"inc_min_ids": 1024, "incremental": 0},
-    "inc_min_ids": {"inc_min_ids": 1024}, "inc_div": {"inc_min_ids": 1024, "inc_div": 1},
-    "inc_inplace": {"inc_min_ids": 1024, "inc_inplace": 0},
+    "seed_refresh": {"seed_refresh": 0.5}, "incremental": {"inc_min_ids": 1024, "incremental": 1},
+    "inc_min_ids": {"inc_min_ids": 1024, "incremental": 1}, "inc_div": {"incremental": 1, "inc_min_ids": 1024, "inc_div": 1},
+    "inc_inplace": {"incremental": 1, "inc_min_ids": 1024, "inc_inplace": 0},
     "refresh_labels": {"refresh_min_batch": 1024, "refresh_labels": 1},
     # the bucketed fold (bucket_fold.h) at this size only when forced by bucket_min_ids / bucket_min_batch
     "bucket": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket": 0},
@@ -554,7 +555,7 @@ KNOB_CASES = {
     "bucket_hub_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_hub_sample": 0.1},
     "lds_edges_per_word": {"lds_edges_per_word": 1e9},  # the short windows take the global-bitmap filter
     "bucket_p2_per": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 12},
-    "inc_check": {"inc_min_ids": 1024, "inc_div": 1, "inc_check": 1},  # diagnostics: checks every incremental compress
+    "inc_check": {"incremental": 1, "inc_min_ids": 1024, "inc_div": 1, "inc_check": 1},  # diagnostics: checks every incremental compress
 }
 
 

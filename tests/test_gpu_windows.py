@@ -93,7 +93,7 @@ def test_c3_incremental_compress_every_window(torch_cuda, name):
     regime of round 2's stale label) and checked by the library itself (inc_check: every incremental
     compress against the roots of the forest it started from, every block's LDS bloom copy against memory), every
     window against the oracle."""
-    stats = fold_windows(torch_cuda, name, knobs={"inc_div": 8, "inc_check": 1})
+    stats = fold_windows(torch_cuda, name, knobs={"incremental": 1, "inc_div": 8, "inc_check": 1})
     checks, bad, lost = stats[0]
     assert checks >= 1 and bad == 0 and lost == 0, stats
 
@@ -105,7 +105,7 @@ def test_c3_default_every_window(torch_cuda):
 def test_c5_every_window(torch_cuda):
     """C5 (path + stars, 2^24 ids) in all 256 windows of 2^16 edges: 256 incremental compresses, each emission
     against the oracle."""
-    stats = fold_windows(torch_cuda, "c5_adversarial/w64K", knobs={"inc_check": 1})
+    stats = fold_windows(torch_cuda, "c5_adversarial/w64K", knobs={"incremental": 1, "inc_check": 1})
     checks, bad, lost = stats[0]
     assert checks >= 200 and bad == 0 and lost == 0, stats
 

@@ -25,7 +25,7 @@ def main():
             W = 1 << wl
             for inc_div in (4, 8, 16, 32, 64, 1 << 30):
                 with DisjointSet(V) as ds:
-                    ds.tune(inc_div=inc_div)
+                    ds.tune(incremental=1, inc_div=inc_div)
                     n_w = min(E // W, 24)
                     for rep in range(2):  # rep 0 warms up (allocations); rep 1 is timed
                         ds.reset()
