@@ -357,6 +357,128 @@ def c2_rotating_leg(local, steps, warmup, digests, tune):
             "roofline": {k: roof[k] for k in ("kernel", "achieved", "frac", "kernel_ms_avg", "pipeline")}}
 
 
+def windows_leg(name, ds_factory, windows, steps, warmup, digest, V, workload_key, note):
+    """One extra workload at N = 1, from edges already in HBM: per step reset + for every window (device pointer,
+    edge count) a fold and an emission (compress). Timed bare, then instrumented steps for the per-kernel stats and
+    the dominant kernel's roofline; parity of the final summary (and, when the fixture has them, of every window of
+    one more step) against the oracle's digests."""
+    import torch
+
+    ds = ds_factory()
+    E = sum(n for _, n in windows)
+
+    def step(check=None):
+        ds.reset()
+        for w, (ptr, n) in enumerate(windows):
+            ds.fold_device(ptr, n)
+            ds.compress()
+            if check is not None:
+                check(w)
+
+    for _ in range(warmup):
+        step()
+    ds.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ds.sync()
+    el = (time.perf_counter() - t0) / steps
+    parity = None
+    if digest is not None:
+        bad = []
+        per_window = digest.get("windows")
+
+        def check(w):
+            if per_window is not None:
+                got, seen, comps = ds.label_digest()
+                want = per_window[w]
+                if (str(got), seen, comps) != (want["digest"], want["seen"], want["components"]):
+                    bad.append(w)
+
+        step(check)
+        got, seen, comps = ds.label_digest()
+        final = digest if per_window is None else per_window[-1]
+        ok = (str(got), seen, comps) == (final["digest"], final["seen"], final["components"]) and not bad
+        parity = ("bit-exact" + (" (every window)" if per_window is not None else "")) if ok else f"MISMATCH {bad}"
+    inst = max(1, min(steps, 3))
+    ds.enable_timing(1)
+    ds.fold_profile()
+    for _ in range(inst):
+        step()
+    kstats, phases, spans = kernel_stats(ds.fold_profile(), V, inst)
+    ds.enable_timing(0)
+    ds.close()
+    roof = make_roofline(kstats, phases, spans, inst, workload_key, "dispatch events, after the timed steps", [])
+    return {"value": E / el, "unit": "edges/s", "ms_per_step": el * 1e3, "windows": len(windows),
+            "ms_per_window": el * 1e3 / len(windows), "edges": E, "steps": steps, "parity": parity, "note": note,
+            "roofline": {k: roof[k] for k in ("kernel", "achieved", "frac", "kernel_ms_avg", "traffic", "traffic_source",
+                                              "pipeline")},
+            "kernels_ms_per_step": {k: round(v["ms_per_step"], 5) for k, v in kstats.items()}}
+
+
+def config_legs(local, steps, warmup, digests, tune, d_edges=None):
+    """Every other bench config of BASELINE.json at N = 1 beside the headline: C4's 1/8
+    share (one rank's fold at N = 8), C4 in 8 windows (the windowed big-id-range path), C5 in 256 windows, C2 in 16
+    windows, C3 in one window and in 1M-edge windows. d_edges: C4's whole stream, already in HBM."""
+    import torch
+
+    from gelly_stream import DisjointSet
+    from gelly_stream import generators as G
+
+    out = {}
+
+    def factory(V):
+        def make():
+            ds = DisjointSet(V, local)
+            if tune:
+                ds.tune(**tune)
+            return ds
+        return make
+
+    def wins(ptr, starts):
+        return [(ptr + 8 * b, e - b) for b, e in zip(starts[:-1], starts[1:])]
+
+    if d_edges is not None:
+        E4, V4 = G.CONFIGS["c4_kron26"].info()
+        base = d_edges.data_ptr()
+        share = 1 << 27
+        try:
+            out["c4_share"] = windows_leg("c4_share", factory(V4), [(base, share)], steps, warmup,
+                                          digests.get("c4_share"), V4, "c4_share",
+                                          "C4's first 2^27 edges into a fresh summary: what each rank folds at N = 8")
+        except Exception as e:
+            out["c4_share"] = {"error": repr(e)}
+        try:
+            w = 1 << 27
+            out["c4_kron26/w8"] = windows_leg("c4_kron26/w8", factory(V4), wins(base, list(range(0, E4 + 1, w))),
+                                              max(2, steps // 4), 1, digests.get("c4_kron26/w8"), V4, "c4_w8",
+                                              "C4 in 8 windows of 2^27 edges, an emission (compress) per window")
+        except Exception as e:
+            out["c4_kron26/w8"] = {"error": repr(e)}
+    for key, cfg_name, wedges in (("c5_adversarial/w64K", "c5_adversarial", 1 << 16),
+                                  ("c2_rmat20/w1M", "c2_rmat20", 1 << 20),
+                                  ("c3_gnm24", "c3_gnm24", 0),
+                                  ("c3_gnm24/w1M", "c3_gnm24", 1 << 20)):
+        try:
+            cfg = G.CONFIGS[cfg_name]
+            E, V = cfg.info()
+            d = torch.empty(2 * E, dtype=torch.int32, device=f"cuda:{local}")
+            G.generate_device(cfg, 0, E, d.data_ptr(), torch.cuda.current_stream(local).cuda_stream)
+            torch.cuda.synchronize()
+            starts = list(range(0, E, wedges)) + [E] if wedges else [0, E]
+            dig = digests.get(key) if key in digests else None
+            if key == "c2_rmat20/w1M":
+                dig = {"digest": digests["c2_rmat20"]["digest"], "seen": digests["c2_rmat20"]["seen"],
+                       "components": digests["c2_rmat20"]["components"]} if "c2_rmat20" in digests else None
+            out[key] = windows_leg(key, factory(V), wins(d.data_ptr(), starts), steps, warmup, dig, V, cfg_name,
+                                   f"{cfg_name} in {len(starts) - 1} window(s), an emission per window")
+            del d
+            torch.cuda.empty_cache()
+        except Exception as e:
+            out[key] = {"error": repr(e)}
+    return out
+
+
 def main():
     args = parse()
     import numpy as np
@@ -523,8 +645,13 @@ def main():
                   if group is not None and merge_ms else None),
     }
     if world == 1 and not args.no_extras:
-        del d_edges
         forest.ds.close()
+        try:
+            result["configs"] = config_legs(local, args.steps, args.warmup, digests, tune,
+                                            d_edges if args.workload == "c4_kron26" else None)
+        except Exception as e:
+            result["configs"] = {"error": repr(e)}
+        del d_edges
         torch.cuda.empty_cache()
         try:
             hf, hl = host_fed_leg(cfg, V, local, args.steps, tune)

@@ -179,9 +179,10 @@ constexpr u32 kSlack = 1u << 12;
 constexpr u32 kChunk = GCC_KCHUNK;
 
 
-__host__ __device__ inline u64 storage_edges(u64 n, u32 ns, u32 blocks) {
-    return n + n / 4 + (u64)ns * (kSlack + 64 + (u64)blocks * kChunk) + 64 +
-           (bk_aligned(n) ? (u64)ns * kBkAlign : 0);
+// The entries `nl` lists of an n-edge batch can claim (each list's capacity rounded up to 16); `aligned`: the buckets'
+// capacities of a batch of >= 2^26 edges are also rounded up to kBkAlign (the v-lists' are not).
+__host__ __device__ inline u64 storage_edges(u64 n, u32 nl, u32 blocks, bool aligned) {
+    return n + n / 4 + (u64)nl * (kSlack + 64 + (u64)blocks * kChunk) + 64 + (aligned ? (u64)nl * kBkAlign : 0);
 }
 
 __device__ __forceinline__ u32 est_cap(u32 hits, u64 n, u64 n_smp, u32 blocks) {

@@ -116,19 +116,32 @@ __device__ __forceinline__ void trace_start(u32 id) {
     }
 }
 
-template <bool REC>
+// SPLIT: path splitting in the finds (plain stores). END: 0 nothing; 1 every block ends with an agent-scope release
+// (its XCD's dirty L2 lines written back before the kernel ends); 2 every wave ends with s_waitcnt vmcnt(0) (its
+// stores and atomics acknowledged before it ends). A/B knobs of the recording fold (tune inc_split / fold_release).
+template <bool REC, bool SPLIT = true, int END = 0>
 __global__ __launch_bounds__(kBlock) void fold_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
                                                       u64 n_edges, u32* __restrict__ bloom, u32 cap,
                                                       u32* __restrict__ err) {
     trace_start(kTrFold);
     NoCount c;
+    typedef gcc::UnionFind<gcc::LoadPlain, SPLIT> U;
     const u64 stride = (u64)gridDim.x * kBlock;
     for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n_edges; i += stride) {
         const u64 e = __builtin_nontemporal_load(edges + i);
         u32 a = (u32)e, b = (u32)(e >> 32);
         if (!edge_ok(a, b, cap, err)) continue;
-        if constexpr (REC) UF::unite(parent, a, b, c, gcc::BloomRec{bloom});
-        else UF::unite(parent, a, b, c);
+        if constexpr (REC) U::unite(parent, a, b, c, gcc::BloomRec{bloom});
+        else U::unite(parent, a, b, c);
+    }
+    if constexpr (END == 1) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    } else if constexpr (END == 2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 }
 
@@ -857,6 +870,46 @@ __global__ __launch_bounds__(kBlock) void inc_verify_kernel(const u32* __restric
             o[3] = r;
             o[4] = marked;
             o[5] = p < n ? pre[p] : UNSEEN;
+        }
+    }
+}
+
+// Diagnostics (tune key post_check, round 4): a check that runs AFTER an incremental compress and changes nothing
+// before or inside it (no copy of the forest, no host sync, no memory-side reads around the compress). For every
+// seen v it tests the compress's output invariant labels[labels[v]] == labels[v]; the first kPostRecs offenders are
+// recorded with what tells the candidate mechanisms apart: whether labels[v] is marked in the bloom the compress used
+// (memory-side read; that bloom stays intact until the next compress clears it), the true root (a walk: the array is
+// quiescent here), and, with post_check 2, the labels after the previous compress (prev: whether labels[v] was
+// already a non-root when the window started, so that no fold of this window could have hooked it).
+// d[0] = offenders (all checks), d[1] = checks run; records at d[16 + 8 k]: check#, v, l, labels[l], root, marked,
+// prev[v], prev[l].
+constexpr u32 kPostRecs = 6;
+__global__ __launch_bounds__(kBlock) void inc_post_check_kernel(const u32* __restrict__ labels, u32 n,
+                                                                const u32* __restrict__ bloom,
+                                                                const u32* __restrict__ prev, u32 check_no,
+                                                                u32* __restrict__ d) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&d[1], 1u);
+    const u32 stride = gridDim.x * kBlock;
+    for (u32 v = blockIdx.x * kBlock + threadIdx.x; v < n; v += stride) {
+        const u32 l = labels[v];
+        if (l == UNSEEN || l >= n) continue;
+        const u32 ll = labels[l];
+        if (ll == l) continue;
+        const u32 k = atomicAdd(&d[0], 1u);
+        if (k < kPostRecs) {
+            u32 r = l;
+            for (u32 hop = 0; hop < 64 && labels[r] < r; ++hop) r = labels[r];
+            const u32 word = __hip_atomic_fetch_or(const_cast<u32*>(bloom) + gcc::bloom_word(l), 0u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+            u32* o = d + 16 + 8 * k;
+            o[0] = check_no;
+            o[1] = v;
+            o[2] = l;
+            o[3] = ll;
+            o[4] = r;
+            o[5] = (word & gcc::bloom_mask(l)) == gcc::bloom_mask(l);
+            o[6] = prev ? prev[v] : UNSEEN;
+            o[7] = prev ? prev[l] : UNSEEN;
         }
     }
 }
@@ -1707,6 +1760,12 @@ struct FoldTune {
     // diagnostics: every incremental compress is checked against the roots of the forest it started from and its
     // bloom LDS copies against memory-side reads; failures go to stderr and to gcc_forest_inc_check_stats
     bool inc_check = false;
+    // diagnostics that leave the compress itself alone: a check kernel after every incremental compress (1), and the
+    // previous labels kept for its records (2); gcc_forest_post_check_stats
+    int post_check = 0;
+    // the recording fold (fold_kernel<true>): path splitting (plain stores) on / off, an agent release at its end
+    bool inc_split = true;
+    int fold_release = 0;
     // bucketed fold of a fresh forest (bucket_fold.h): batches of >= bucket_min_batch edges over >= bucket_min_ids
     // ids (default: exactly the forests whose giant bitmap does not fit LDS); seeding = bucket_levels P2 + P3 levels
     // over the first bucket_sample of every bucket
@@ -1768,6 +1827,9 @@ struct gcc_forest {
     u32* d_dbg = nullptr;  // tune inc_check: 64 words (compress_inc_kernel<.., true>, inc_verify_kernel)
     u32* h_dbg = nullptr;
     u64 inc_checks = 0, inc_bad_labels = 0, inc_lost_marks = 0;
+    u32* d_post = nullptr;  // tune post_check: inc_post_check_kernel's counters and records (64 words)
+    u32* d_prev = nullptr;  // post_check 2: the labels after the previous checked compress
+    u32 post_checks = 0;
 
     // pinned double-buffered staging for host-fed edges (per-edge foldEdges appends here)
     static constexpr u64 kStageEdges = 1ull << 20;  // 8 MiB per slot
@@ -2000,6 +2062,26 @@ static int inc_check_end(gcc_forest* h, const u32* pre, const u32* labels, const
     return GCC_OK;
 }
 
+// tune post_check (diagnostics): inc_post_check_kernel after the incremental compress, stream-ordered, no sync; with
+// post_check 2 the labels are also copied into d_prev after the check (for the next check's records)
+static int post_check_launch(gcc_forest* h, const u32* labels, const u32* bloom) {
+    if (!h->d_post) {
+        HIP_TRY(hipMalloc((void**)&h->d_post, 64 * sizeof(u32)));
+        HIP_TRY(hipMemsetAsync(h->d_post, 0, 64 * sizeof(u32), h->stream));
+    }
+    const bool keep = h->tune.post_check >= 2;
+    if (keep && !h->d_prev) {
+        HIP_TRY(hipMalloc((void**)&h->d_prev, (size_t)h->cap * sizeof(u32)));
+        HIP_TRY(hipMemsetAsync(h->d_prev, 0xFF, (size_t)h->cap * sizeof(u32), h->stream));
+    }
+    hipLaunchKernelGGL(inc_post_check_kernel, dim3(kMaxGrid), dim3(kBlock), 0, h->stream, labels, h->cap, bloom,
+                       (const u32*)(keep ? h->d_prev : nullptr), h->post_checks++, h->d_post);
+    HIP_TRY(hipGetLastError());
+    if (keep)
+        HIP_TRY(hipMemcpyAsync(h->d_prev, labels, (size_t)h->cap * sizeof(u32), hipMemcpyDeviceToDevice, h->stream));
+    return GCC_OK;
+}
+
 // compress into the spare buffer and swap; with the filter on, refresh the giant bitmap from the new labels.
 // Incremental (compress_inc_kernel) when every mutation since the last compress was recorded.
 // oth (the merge encode): a full compress also writes the others mask of every 64-id word (chunk_oth); returns
@@ -2056,6 +2138,7 @@ static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth =
             }
             // the forest the compress started from: the copy in d_spare (in place), or d_parent itself
             if (!rc && check) rc = inc_check_end(h, inplace ? h->d_spare : h->d_parent, out, bl);
+            if (!rc && h->tune.post_check) rc = post_check_launch(h, out, bl);
         } else if (!rc) {
             rc = launch_k(h, name, 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)), dim3(kBlock), 0,
                           h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
@@ -2096,9 +2179,21 @@ static int refresh_now(gcc_forest* h) {
 static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* name) {
     if (n == 0) return GCC_OK;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
-    if (h->rec_all && n * std::max<u64>(1, h->tune.inc_div) <= (u64)h->cap)
-        return launch_k(h, name, n, fold_kernel<true>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent, edges,
-                        n, h->bloom(h->bloom_cur), h->cap, h->d_err);
+    if (h->rec_all && n * std::max<u64>(1, h->tune.inc_div) <= (u64)h->cap) {
+        const dim3 g(grid_for(n, kMaxGrid));
+        u32* bl = h->bloom(h->bloom_cur);
+        const int v = (h->tune.inc_split ? 0 : 1) + 2 * std::max(0, std::min(2, h->tune.fold_release));
+#define GCC_REC(S, E) launch_k(h, name, n, fold_kernel<true, S, E>, g, dim3(kBlock), 0, h->d_parent, edges, n, bl, h->cap, h->d_err)
+        switch (v) {
+        case 0: return GCC_REC(true, 0);
+        case 1: return GCC_REC(false, 0);
+        case 2: return GCC_REC(true, 1);
+        case 3: return GCC_REC(false, 1);
+        case 4: return GCC_REC(true, 2);
+        default: return GCC_REC(false, 2);
+        }
+#undef GCC_REC
+    }
     h->rec_all = false;
     return launch_k(h, name, n, fold_kernel<false>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent, edges, n,
                     (u32*)nullptr, h->cap, h->d_err);
@@ -2297,12 +2392,12 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     }
     const u32 p1_blocks = 2 * (u32)h->n_cu;  // (bucket_p1 = 1 runs n_cu blocks: fewer writers, same slack bound)
     const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
-    const u64 bk_S = bk::bk_entries(bk::storage_edges(n, ns, p1_blocks));  // entries (a multiple of 2^19)
+    const u64 bk_S = bk::bk_entries(bk::storage_edges(n, ns, p1_blocks, bk::bk_aligned(n)));  // entries (a multiple of 2^19)
     if ((rc = grow(h->d_bk, h->bk_cap_bytes, bk::bk_bytes(bk_S), h->stream))) return rc;
     u32* bk_lo = reinterpret_cast<u32*>(h->d_bk);
     bk::u16* bk_hi = reinterpret_cast<bk::u16*>(h->d_bk + 4 * bk_S);
     if ((rc = grow(h->d_ovf, h->ovf_cap, n / 8 + 65536, h->stream))) return rc;
-    const u64 vl_S = bk::vl_entries(bk::storage_edges(n, ns, p2_blocks));
+    const u64 vl_S = bk::vl_entries(bk::storage_edges(n, bk::vslices(h->cap), p2_blocks, false));
     if ((rc = grow(h->d_vl, h->vl_cap, bk::vl_bytes(vl_S), h->stream))) return rc;
     const bk::VList vl{reinterpret_cast<bk::u16*>(h->d_vl), h->d_vl + 2 * vl_S};
     // room for half the batch in the slow lists (C4: 3.9 % slow; C4's 1/8 share: more than the 12.5 % an n/8
@@ -2886,6 +2981,8 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (h->d_bits) (void)hipFree(h->d_bits);
     if (h->d_bloom) (void)hipFree(h->d_bloom);
     if (h->d_dbg) (void)hipFree(h->d_dbg);
+    if (h->d_post) (void)hipFree(h->d_post);
+    if (h->d_prev) (void)hipFree(h->d_prev);
     if (h->h_dbg) (void)hipHostFree(h->h_dbg);
     if (h->d_giant) (void)hipFree(h->d_giant);
     if (h->d_flags) (void)hipFree(h->d_flags);
@@ -3554,6 +3651,9 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "inc_min_ids") t.inc_min_ids = (u64)value;
     else if (k == "inc_div") t.inc_div = std::max<u64>(1, (u64)value);
     else if (k == "inc_check") t.inc_check = value != 0;
+    else if (k == "inc_split") t.inc_split = value != 0;
+    else if (k == "fold_release") t.fold_release = (int)value;
+    else if (k == "post_check") t.post_check = std::max(0, std::min(2, (int)value));
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(2, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
@@ -3635,6 +3735,24 @@ int gcc_forest_inc_check_stats(gcc_forest* h, uint64_t* checks, uint64_t* bad_la
     *checks = h->inc_checks;
     *bad_labels = h->inc_bad_labels;
     *lost_marks = h->inc_lost_marks;
+    return GCC_OK;
+}
+
+int gcc_forest_post_check_stats(gcc_forest* h, uint64_t* checks, uint64_t* offenders, uint32_t* records,
+                                uint32_t n_records) {
+    CHECK_ARG(h && checks && offenders, "null argument");
+    *checks = 0;
+    *offenders = 0;
+    if (!h->d_post) return GCC_OK;
+    DeviceGuard g(h->device);
+    u32 d[64];
+    HIP_TRY(hipMemcpyAsync(d, h->d_post, sizeof(d), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    *checks = d[1];
+    *offenders = d[0];
+    if (records)
+        for (u32 k = 0; k < std::min<u32>(n_records, std::min<u32>(d[0], kPostRecs)); ++k)
+            std::memcpy(records + 8 * k, d + 16 + 8 * k, 8 * sizeof(u32));
     return GCC_OK;
 }
 

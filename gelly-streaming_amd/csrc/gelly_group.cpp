@@ -106,6 +106,11 @@ struct gcc_comm {
     void* d_recv = nullptr;
     u64 recv_bytes = 0;
     u32* h_hdr = nullptr;  // pinned: the gathered headers (4 u32 per rank)
+    // the status exchange (agree()): 16 B per rank gathered, + this rank's 16 B to send; allocated at init, so a
+    // rank can always take part in it
+    void* d_status = nullptr;
+    u32* h_status = nullptr;
+    u64 agreed_msg = 0;  // the message size every rank has buffers for (the same value on every rank)
     u64 cap_others = 0;    // the speculative list capacity (grows on overflow, shrinks slowly)
     bool prefer_labels = false;
     u64 last_bytes = 0;    // bytes each rank contributed to the last merge's all_gather
@@ -118,12 +123,14 @@ struct gcc_comm {
 
 namespace {
 
+// Grow a buffer. The new one is allocated before the old one is freed, so a failed allocation leaves the buffer as it
+// was: every rank's buffers stay at least as large as the sizes the ranks last agreed on (gcc_comm::agreed_msg).
 int ensure(void*& p, u64& have, u64 need) {
     if (have >= need) return GCC_OK;
-    if (p) HIP_TRY(hipFree(p));
-    p = nullptr;
-    have = 0;
-    HIP_TRY(hipMalloc(&p, (size_t)need));
+    void* q = nullptr;
+    HIP_TRY(hipMalloc(&q, (size_t)need));
+    if (p) (void)hipFree(p);
+    p = q;
     have = need;
     return GCC_OK;
 }
@@ -145,12 +152,58 @@ int fail_comm(gcc_comm* c, int rc) {
     return rc;
 }
 
-// The label-array exchange (no dominant component): all_gather of the canonical labels, absorb the others.
-int merge_labels_rccl(gcc_forest* h, gcc_comm* c, u32 V, hipStream_t st) {
+int alloc_status(gcc_comm* c) {
+    DeviceGuard g(c->device);
+    HIP_TRY(hipMalloc(&c->d_status, (size_t)(c->nranks + 1) * 16));
+    HIP_TRY(hipHostMalloc((void**)&c->h_status, (size_t)(c->nranks + 1) * 16, hipHostMallocDefault));
+    return GCC_OK;
+}
+
+// The ranks agree before a collective whose inputs a rank may have failed to produce (a buffer it could not
+// allocate, an absorb or compress that failed after its header had gone out): one all_gather of a 16-B status word
+// per rank. Every rank reads the same words, so either all of them go on to the collective or all of them return
+// (the communicator stays usable). *failed = the first failed rank, or -1. Only a failure of this exchange itself
+// aborts the communicator.
+int agree(gcc_comm* c, hipStream_t st, int local_rc, int* failed) {
+    *failed = -1;
+    u32* mine = c->h_status + 4 * c->nranks;
+    mine[0] = local_rc ? GCC_MSG_STATUS_FAILED : 0u;
+    mine[1] = (u32)local_rc;
+    mine[2] = mine[3] = 0;
+    char* d_mine = static_cast<char*>(c->d_status) + (u64)16 * c->nranks;
+    if (hipMemcpyAsync(d_mine, mine, 16, hipMemcpyHostToDevice, st) != hipSuccess)
+        return fail_comm(c, gcc_set_err(GCC_E_HIP, "status word copy: %s", hipGetErrorString(hipGetLastError())));
+    const ncclResult_t r = rccl().AllGather(d_mine, c->d_status, 16, ncclUint8, c->comm, st);
+    if (r != ncclSuccess)
+        return fail_comm(c, gcc_set_err(GCC_E_HIP, "ncclAllGather (status): %s", rccl().GetErrorString(r)));
+    if (hipMemcpyAsync(c->h_status, c->d_status, (size_t)16 * c->nranks, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return fail_comm(c, gcc_set_err(GCC_E_HIP, "status words: %s", hipGetErrorString(hipGetLastError())));
+    for (int p = 0; p < c->nranks; ++p)
+        if (c->h_status[4 * p] == GCC_MSG_STATUS_FAILED) {
+            *failed = p;
+            break;
+        }
+    return GCC_OK;
+}
+
+// local_rc (this rank's own error, or 0) and the peers' statuses -> the error every rank returns, or 0
+int agreed_error(int local_rc, int failed) {
+    if (local_rc) return local_rc;
+    if (failed >= 0) return gcc_set_err(GCC_E_INTERNAL, "group merge: rank %d failed (its error is on that rank)", failed);
+    return GCC_OK;
+}
+
+// The label-array exchange (no dominant component): all_gather of the canonical labels, absorb the others. The ranks
+// agree first (a rank may arrive here with an error from the compact rounds, or fail to get its labels or buffer).
+int merge_labels_rccl(gcc_forest* h, gcc_comm* c, u32 V, hipStream_t st, int local_rc) {
     const u32* lab = nullptr;
-    int rc = gcc_forest_labels_device(h, &lab);
+    int rc = local_rc;
+    if (!rc) rc = gcc_forest_labels_device(h, &lab);
     if (!rc) rc = ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * V * sizeof(u32));
-    if (rc) return fail_comm(c, rc);  // before the collective: the peers cannot learn of it
+    int failed = -1;
+    ABI_TRY(agree(c, st, rc, &failed));
+    if (rc || failed >= 0) return agreed_error(rc, failed);
     const ncclResult_t r = rccl().AllGather(lab, c->d_recv, V, ncclUint32, c->comm, st);
     if (r != ncclSuccess)
         return fail_comm(c, gcc_set_err(GCC_E_HIP, "ncclAllGather (labels): %s", rccl().GetErrorString(r)));
@@ -193,6 +246,11 @@ int gcc_comm_init(int device, int nranks, int rank, const void* id, gcc_comm** o
         delete c;
         return gcc_set_err(GCC_E_HIP, "ncclCommInitRank: %s", rccl().GetErrorString(r));
     }
+    const int rc = alloc_status(c);
+    if (rc) {
+        (void)gcc_comm_destroy(c);
+        return rc;
+    }
     *out = c;
     return GCC_OK;
 }
@@ -211,6 +269,7 @@ int gcc_comm_init_all(int ndev, const int* devices, gcc_comm** comms_out) {
         c->rank = i;
         comms_out[i] = c;
     }
+    for (int i = 0; i < ndev; ++i) ABI_TRY(alloc_status(comms_out[i]));
     return GCC_OK;
 }
 
@@ -220,6 +279,8 @@ int gcc_comm_destroy(gcc_comm* c) {
     if (c->d_send) (void)hipFree(c->d_send);
     if (c->d_recv) (void)hipFree(c->d_recv);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
+    if (c->d_status) (void)hipFree(c->d_status);
+    if (c->h_status) (void)hipHostFree(c->h_status);
     if (c->comm) (void)rccl().CommDestroy(c->comm);
     delete c;
     return GCC_OK;
@@ -248,9 +309,10 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
     if (!c->h_hdr) HIP_TRY(hipHostMalloc((void**)&c->h_hdr, (size_t)c->nranks * 16, hipHostMallocDefault));
     if (c->cap_others == 0) c->cap_others = std::max<u64>(1024, V / 64);
     c->last_rounds = 0;
-    // Every rank takes the same decisions (sizes, repeats) from the gathered headers. A rank whose own encode or
-    // absorb fails keeps following them and sends a failed-status header (include/gelly_cc.h) in the next round,
-    // so every rank leaves the loop together with an error instead of one rank leaving its peers in a collective.
+    // Every rank takes the same decisions (sizes, repeats) from the gathered headers. A rank whose own encode, absorb
+    // or compress fails keeps following them: in a next compact round it sends a failed-status header
+    // (include/gelly_cc.h), before a round that grows the buffers and before the label exchange the ranks agree
+    // (agree()), so every rank leaves together with an error instead of one rank leaving its peers in a collective.
     int local_rc = GCC_OK;
     while (!c->prefer_labels) {
         const u64 cap = c->cap_others;
@@ -259,9 +321,17 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
             c->prefer_labels = true;
             break;
         }
-        int rc = ensure(c->d_send, c->send_bytes, size);
-        if (!rc) rc = ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * size);
-        if (rc) return fail_comm(c, rc);
+        // the buffers grow at the same rounds on every rank (sizes follow the gathered headers): the ranks agree on
+        // the allocation before the all_gather that needs it
+        if (size > c->agreed_msg) {
+            int rc = ensure(c->d_send, c->send_bytes, size);
+            if (!rc) rc = ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * size);
+            int failed = -1;
+            ABI_TRY(agree(c, st, rc ? rc : local_rc, &failed));
+            if (rc || failed >= 0) return agreed_error(rc ? rc : local_rc, failed);
+            c->agreed_msg = size;
+        }
+        int rc = GCC_OK;
         if (!local_rc) local_rc = gcc_forest_encode(h, c->d_send, cap);
         if (local_rc) {  // a header the absorb skips (id_capacity 0) and every rank reads as "the merge failed"
             const u32 hdr[4] = {0xFFFFFFFFu, 0, 0, GCC_MSG_STATUS_FAILED};
@@ -296,8 +366,7 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
         c->cap_others = std::max<u64>(3 * nmax / 2, 2 * cap);  // some list did not fit: again, larger
     }
     ++c->last_rounds;
-    if (local_rc) return fail_comm(c, local_rc);
-    return merge_labels_rccl(h, c, V, st);
+    return merge_labels_rccl(h, c, V, st, local_rc);
 }
 
 // Single process, n forests (SummaryTreeReduce's partials, or one forest per GPU of a process that drives several

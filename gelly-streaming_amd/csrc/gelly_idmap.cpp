@@ -72,17 +72,35 @@ int gcc_idmap_size(gcc_idmap* m, uint64_t* n) {
 
 int gcc_idmap_map(gcc_idmap* m, const int64_t* ids, uint64_t n, uint32_t* dense_out) {
     if (!m || ((!ids || !dense_out) && n)) return gcc_set_err(GCC_E_INVALID, "gcc_idmap_map: null argument");
+    // All or nothing: a batch whose new ids do not all fit leaves the dictionary as it was (a caller that retries or
+    // fails the batch must not find dense ids that were never submitted). The slots this call filled are undone in
+    // reverse order, which restores the linear-probing table exactly (no entry placed earlier probed past them).
+    const uint64_t first_new = m->orig.size();
+    std::vector<uint64_t> filled;
+    auto undo = [&]() {
+        for (auto it = filled.rbegin(); it != filled.rend(); ++it) m->used[*it] = 0;
+        m->orig.resize(first_new);
+    };
     for (uint64_t i = 0; i < n; ++i) {
         const int64_t k = ids[i];
         uint64_t s = mix64((uint64_t)k) & m->mask;
         while (m->used[s] && m->keys[s] != k) s = (s + 1) & m->mask;
         if (!m->used[s]) {  // first sight: the next dense id
-            if (m->orig.size() >= m->capacity)
-                return gcc_set_err(GCC_E_INVALID, "gcc_idmap_map: more than %u distinct vertex ids", m->capacity);
+            if (m->orig.size() >= m->capacity) {
+                undo();
+                return gcc_set_err(GCC_E_INVALID, "gcc_idmap_map: more than %u distinct vertex ids (the batch was not mapped)",
+                                   m->capacity);
+            }
+            try {
+                filled.push_back(s);
+                m->orig.push_back(k);
+            } catch (...) {
+                undo();
+                return gcc_set_err(GCC_E_OOM, "gcc_idmap_map: out of host memory");
+            }
             m->used[s] = 1;
             m->keys[s] = k;
-            m->vals[s] = (uint32_t)m->orig.size();
-            m->orig.push_back(k);
+            m->vals[s] = (uint32_t)(m->orig.size() - 1);
         }
         dense_out[i] = m->vals[s];
     }

@@ -175,7 +175,11 @@ class LiteralCandidates:
         """``new Candidates(true)`` (:31-34). entry_capacity bounds the entries (default 4 x id_capacity, >= 4096)."""
         self.id_capacity = int(id_capacity)
         self.device = int(device)
-        self.entry_capacity = int(entry_capacity or max(4096, 4 * self.id_capacity))
+        if entry_capacity is None:  # the default, clamped to what the C ABI's u32 argument can carry
+            entry_capacity = min(0xFFFFFFFF, max(4096, 4 * self.id_capacity))
+        self.entry_capacity = int(entry_capacity)
+        if not 0 < self.entry_capacity <= 0xFFFFFFFF:
+            raise ValueError(f"entry_capacity {self.entry_capacity} does not fit the C ABI's u32 (1 .. 2^32 - 1)")
         h = c_void_p()
         call("gcc_literal_create", self.device, self.id_capacity, self.entry_capacity, byref(h))
         self._h = h

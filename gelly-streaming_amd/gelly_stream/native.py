@@ -102,6 +102,7 @@ _SIGS = {
     "gcc_forest_tune": (c_int, [c_void_p, c_char_p, ctypes.c_double]),
     "gcc_forest_label_digest": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),
     "gcc_forest_inc_check_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),
+    "gcc_forest_post_check_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), c_void_p, c_uint32]),
     "gcc_msg_bytes": (c_uint64, [c_uint32, c_uint64]),
     "gcc_forest_encode": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_forest_absorb": (c_int, [c_void_p, c_void_p, c_uint64]),

@@ -320,6 +320,15 @@ class DisjointSet:
         call("gcc_forest_inc_check_stats", self.handle, byref(a), byref(b), byref(c))
         return a.value, b.value, c.value
 
+    def post_check_stats(self) -> tuple:
+        """Diagnostics (tune(post_check=1 or 2)): (checks, offenders, records) of the check after every incremental
+        compress; records = up to 6 tuples (check#, v, label, label's label, root, marked, prev[v], prev[label])."""
+        a, b = c_uint64(), c_uint64()
+        rec = (c_uint32 * 48)()
+        call("gcc_forest_post_check_stats", self.handle, byref(a), byref(b), rec, 6)
+        n = min(int(b.value), 6)
+        return a.value, b.value, [tuple(rec[8 * k:8 * k + 8]) for k in range(n)]
+
     def copy(self) -> "DisjointSet":
         """A fresh forest with the same partition (Flink copies the fold's initial value per window)."""
         d = DisjointSet(self.id_capacity, self.device)

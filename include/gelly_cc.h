@@ -254,6 +254,13 @@ int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size);
  * labels that differed from the roots of the forest the compress started from, bloom words whose LDS copy lacked a
  * mark that memory held. Checked compresses synchronise; never on in a timed region. */
 int gcc_forest_inc_check_stats(gcc_forest* h, uint64_t* checks, uint64_t* bad_labels, uint64_t* lost_marks);
+/* diagnostics (tune key post_check = 1 or 2): a kernel after every incremental compress (nothing added before or
+ * inside it, no synchronisation) checks labels[labels[v]] == labels[v] for every seen v. Returns the checks run and
+ * the offenders; `records` (n_records x 8 u32, may be null) receives the first ones: check number, v, label, the
+ * label's own label, the true root, whether the label is marked in the compress's bloom (memory-side read), and with
+ * post_check 2 the previous compress's labels of v and of the label (UNSEEN otherwise). Synchronises. */
+int gcc_forest_post_check_stats(gcc_forest* h, uint64_t* checks, uint64_t* offenders, uint32_t* records,
+                                uint32_t n_records);
 /* ---- id dictionary: Java Long vertex ids at the boundary (host-only, gelly_idmap.cpp) ----
  * DisjointSet<Long> (…/summaries/DisjointSet.java:30-34) is keyed by any Long; the device forest by dense u32
  * ids. The dictionary assigns dense ids in first-seen order and maps a forest's labels over dense ids back to
@@ -262,7 +269,8 @@ typedef struct gcc_idmap gcc_idmap;
 int gcc_idmap_create(uint32_t capacity, gcc_idmap** out); /* at most `capacity` distinct ids */
 int gcc_idmap_destroy(gcc_idmap* m);
 int gcc_idmap_size(gcc_idmap* m, uint64_t* n_ids);
-/* dense_out[i] = dense id of ids[i] (a new id takes the next one); GCC_E_INVALID past the capacity */
+/* dense_out[i] = dense id of ids[i] (a new id takes the next one); GCC_E_INVALID past the capacity. All or nothing:
+ * on an error the dictionary is left exactly as before the call (no id of the batch is mapped) */
 int gcc_idmap_map(gcc_idmap* m, const int64_t* ids, uint64_t n, uint32_t* dense_out);
 int gcc_idmap_lookup(gcc_idmap* m, int64_t id, uint32_t* dense); /* GCC_UNSEEN if never mapped */
 int gcc_idmap_ids(gcc_idmap* m, int64_t* out, uint64_t n);        /* out[d] = original id of dense id d */

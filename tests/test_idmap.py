@@ -37,6 +37,21 @@ def test_first_seen_order_and_lookup():
     d.close()
 
 
+def test_overflowing_batch_maps_nothing():
+    """a batch whose new ids do not all fit is rejected whole: no id of it gets a dense id (a caller that
+    retries or drops the batch must not find mapped ids that were never folded), and the table stays consistent."""
+    d = IdDictionary(10)
+    assert d.map(list(range(100, 108))).tolist() == list(range(8))
+    with pytest.raises(GellyCCError):
+        d.map([100, 5, 6, 101, 7])  # three new ids, room for two
+    assert len(d) == 8
+    assert all(d.lookup(x) is None for x in (5, 6, 7))
+    assert all(d.lookup(100 + i) == i for i in range(8))
+    assert d.map([6, 104, 5]).tolist() == [8, 4, 9]  # the same ids fit once the batch does
+    assert d.ids().tolist() == list(range(100, 108)) + [6, 5]
+    d.close()
+
+
 def test_capacity_is_enforced():
     d = IdDictionary(3)
     d.map([1, 2, 3, 1, 2])
