@@ -305,13 +305,15 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
 // Block-wide exclusive scan of the counts cnt[0..ns), each rounded up to a multiple of 4 (pad4: the runs' padded
 // lengths), into start[] (BLOCK threads, ns <= kMaxBuckets). One barrier inside.
 __device__ __forceinline__ u32 pad4(u32 c) { return (c + 3) & ~3u; }
-template <int BLOCK>
+template <u32 W>
+__device__ __forceinline__ u32 padw(u32 c) { return (c + W - 1) & ~(W - 1); }
+template <int BLOCK, u32 W = 4>
 __device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u32* s_wsum) {
     const u32 per = (ns + BLOCK - 1) / BLOCK;
     u32 loc = 0;
     for (u32 j = 0; j < per; ++j) {
         const u32 s = threadIdx.x * per + j;
-        loc += s < ns ? pad4(cnt[s]) : 0;
+        loc += s < ns ? padw<W>(cnt[s]) : 0;
     }
     const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     u32 inc = loc;
@@ -327,7 +329,7 @@ __device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u
         const u32 s = threadIdx.x * per + j;
         if (s < ns) {
             start[s] = run;
-            run += pad4(cnt[s]);
+            run += padw<W>(cnt[s]);
         }
     }
 }
@@ -341,9 +343,13 @@ __device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u
 // P1's dynamic LDS: the tile in bucket order, every bucket's run padded to a multiple of 4 — up to three slots per
 // slice beyond the tile. (Round 2 first sized it to the tile alone: a full tile's last padded slots fell past the
 // allocation and relied on the LDS allocation's rounding slack; a 1024 x 8 geometry with less slack lost edges.)
-constexpr size_t p1_lds(int block, int per, u32 maxb = 256) { return ((size_t)block * per + 3 * maxb) * sizeof(u64); }
+// W (round 4): entries per lane in the write-out, every run padded to a multiple of W. W = 4: 16 B of lo and 8 B of hi
+// per lane; W = 8: 2 x 16 B of lo and 16 B of hi (8-B stores run at 0.54-0.70x the 16-B rate, MI355X_MICROARCH.md)
+constexpr size_t p1_lds(int block, int per, u32 maxb = 256, u32 w = 4) {
+    return ((size_t)block * per + (w - 1) * maxb) * sizeof(u64);
+}
 
-template <int P1B, int P1P, u32 MAXB = 256>
+template <int P1B, int P1P, u32 MAXB = 256, u32 W = 4>
 __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                           Meta* __restrict__ m, u32* __restrict__ bk_lo,
                                                           u16* __restrict__ bk_hi, u64* __restrict__ ovf, u32 ovf_cap,
@@ -420,9 +426,9 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
         GCC_PH_MARK(phc, 3);
         // every bucket's run is padded to a multiple of 4 with ~0 entries (P2 skips them), so that runs, tile
         // slots and list positions stay multiples of 4 and the write-out moves 4 entries per lane (16 B of lo, 8 of hi)
-        count_scan<P1B>(s_cnt, s_start, ns, s_wsum);
+        count_scan<P1B, W>(s_cnt, s_start, ns, s_wsum);
         for (u32 s = threadIdx.x; s < ns; s += P1B) {
-            const u32 pc = pad4(s_cnt[s]);
+            const u32 pc = padw<W>(s_cnt[s]);
             if (pc) reserve_run(runs, s, pc, &m->bk_cur[s], s_cap[s]);
             for (u32 j = s_cnt[s]; j < pc; ++j) s_srt[s_start[s] + j] = ~0ull;
         }
@@ -434,20 +440,36 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
         GCC_PH_MARK(phc, 5);  // scatter
         __syncthreads();
         GCC_PH_MARK(phc, 6);
-        const u32 tot4 = (s_start[ns - 1] + pad4(s_cnt[ns - 1])) / 4;
-        for (u32 x4 = threadIdx.x; x4 < tot4; x4 += P1B) {
-            const u64x2 ea = reinterpret_cast<const u64x2*>(s_srt)[2 * x4];      // slot 4 x4 is never padding
-            const u64x2 eb = reinterpret_cast<const u64x2*>(s_srt)[2 * x4 + 1];
-            const u64 e[4] = {ea.x, ea.y, eb.x, eb.y};
+        const u32 totw = (s_start[ns - 1] + padw<W>(s_cnt[ns - 1])) / W;
+        for (u32 xw = threadIdx.x; xw < totw; xw += P1B) {
+            u64 e[W];
+#pragma unroll
+            for (u32 k = 0; k < W / 2; ++k) {  // slot W xw is never padding
+                const u64x2 ek = reinterpret_cast<const u64x2*>(s_srt)[(W / 2) * xw + k];
+                e[2 * k] = ek.x;
+                e[2 * k + 1] = ek.y;
+            }
             const u32 s = (u32)e[0] >> kSliceBits;
-            const u32 off = run_pos(runs, s, 4 * x4 - s_start[s]);  // a multiple of 4: all four in one chunk
+            const u32 off = run_pos(runs, s, W * xw - s_start[s]);  // a multiple of W: all W in one chunk
             if (off != 0xFFFFFFFFu) {
-                const u4 lo = {bk_lo_of(e[0]), bk_lo_of(e[1]), bk_lo_of(e[2]), bk_lo_of(e[3])};
-                const u16x4 hi = {bk_hi_of(e[0]), bk_hi_of(e[1]), bk_hi_of(e[2]), bk_hi_of(e[3])};
-                *reinterpret_cast<u4*>(bk_lo + s_base[s] + off) = lo;     // 16-B aligned (bases: 16-entry multiples)
-                *reinterpret_cast<u16x4*>(bk_hi + s_base[s] + off) = hi;  // 8-B aligned
+#pragma unroll
+                for (u32 k = 0; k < W / 4; ++k) {  // 16-B aligned (bases: 16-entry multiples)
+                    const u4 lo = {bk_lo_of(e[4 * k]), bk_lo_of(e[4 * k + 1]), bk_lo_of(e[4 * k + 2]), bk_lo_of(e[4 * k + 3])};
+                    *reinterpret_cast<u4*>(bk_lo + s_base[s] + off + 4 * k) = lo;
+                }
+                if constexpr (W == 8) {
+                    typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+                    const u16x8 hi = {bk_hi_of(e[0]), bk_hi_of(e[1]), bk_hi_of(e[2]), bk_hi_of(e[3]),
+                                      bk_hi_of(e[4]), bk_hi_of(e[5]), bk_hi_of(e[6]), bk_hi_of(e[7])};
+                    *reinterpret_cast<u16x8*>(bk_hi + s_base[s] + off) = hi;  // 16-B aligned
+                } else {
+                    const u16x4 hi = {bk_hi_of(e[0]), bk_hi_of(e[1]), bk_hi_of(e[2]), bk_hi_of(e[3])};
+                    *reinterpret_cast<u16x4*>(bk_hi + s_base[s] + off) = hi;  // 8-B aligned
+                }
             } else {  // the bucket is full (its estimate was low): the overflow list (folded at the end)
-                const u32 k = 1u + (e[1] != ~0ull) + (e[2] != ~0ull) + (e[3] != ~0ull);  // padding only at the end
+                u32 k = 1;
+#pragma unroll
+                for (u32 i = 1; i < W; ++i) k += e[i] != ~0ull;  // padding only at the end
                 const u32 o = atomicAdd(&m->ovf_cur, k);
                 for (u32 i = 0; i < k; ++i)
                     if (o + i < ovf_cap) ovf[o + i] = e[i];

@@ -582,8 +582,9 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
         }
     };
     if (wave < nfull) load_batch(wave);
-    if (bloom_clear)  // the bloom buffer the next fold records into (compress_inc_kernel)
-        for (u32 w = blockIdx.x * kBlock + threadIdx.x; w < gcc::kBloomBits / 32; w += gridDim.x * kBlock) bloom_clear[w] = 0;
+    if (bloom_clear)  // the bloom buffer the next fold records into (compress_inc_kernel): memory-side atomics
+        for (u32 w = blockIdx.x * kBlock + threadIdx.x; w < gcc::kBloomBits / 32; w += gridDim.x * kBlock)
+            atomicAnd(&bloom_clear[w], 0u);
     if (threadIdx.x == 0) {
         const u32 g0 = giant_prev ? *giant_prev : UNSEEN;
         s_g = (g0 == UNSEEN) ? UNSEEN : UF::find_from(parent, g0, parent[g0], c);
@@ -700,9 +701,10 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
         const u32x4* src = reinterpret_cast<const u32x4*>(bloom);
         u32x4* dst = reinterpret_cast<u32x4*>(s_bloom);
         lds_fill<kIncBlock>(dst, src, kW4);
+        // the other bloom is cleared with memory-side atomics, never with plain stores: the next fold's marks are
+        // memory-side atomics, and a plain store of this kernel can still land after the next kernel's atomics
         const u32 per = (kW4 + gridDim.x - 1) / gridDim.x, a = blockIdx.x * per, b = min(kW4, a + per);
-        const u32x4 z = {0, 0, 0, 0};
-        for (u32 w = a + threadIdx.x; w < b; w += kIncBlock) reinterpret_cast<u32x4*>(bloom_clear)[w] = z;
+        for (u32 w = 4 * a + threadIdx.x; w < 4 * b; w += kIncBlock) atomicAnd(&bloom_clear[w], 0u);
     }
     if (threadIdx.x == 0) {
         NoCount c;
@@ -1402,7 +1404,7 @@ __global__ void msg_header_kernel(u32* __restrict__ hdr, const u32* __restrict__
 //    (bitmap `mine`, root R; valid forever since components only grow)? If so, witness[p] = one shared id.
 //  msg_absorb_bits_kernel: an overlapping peer's giant G_p is connected to T (root R) through the witness, so
 //    the union U of their bitmaps only needs its ids OUTSIDE T joined to R, each ONCE however many peers hold it
-//    (one 64-id word per wave, one id per lane); a new id above R by a plain store;
+//    (one 64-id word per wave, one id per lane); a new id above R by one CAS (or deferred to the compress);
 //  msg_absorb_kernel: the giants without overlap (or all of them when there is no T: id by id against their
 //    own root), then the (v, label) lists.
 constexpr u32 kMaxPeers = 64;
@@ -1457,9 +1459,10 @@ __device__ __forceinline__ void msg_peers(const char* __restrict__ msgs, u64 str
 
 // Absorb, phase 1 (after msg_overlap_kernel): the union U of the giants that meet T, minus T, one 64-id word per
 // wave, each id once however many peers hold it. Every id of such a giant is connected to T (through the
-// witness), so x in U \ T joins T's root R. A new id above R — the common case — is hung under R by a PLAIN
-// store: in this kernel x has no other writer (each id belongs to one lane, and the other lanes' unions only
-// CAS roots of trees of seen ids), and the witness and list unions, which could also touch it, run in phase 2.
+// witness), so x in U \ T joins T's root R. A new id above R — the common case — is hung under R by ONE CAS
+// (UNSEEN -> R). Round 1-3 used a plain store (in this kernel x has no other writer), but phase 2's list unions may
+// CAS the same slot in the next kernel, and on gfx950 a plain store can land after the next kernel's memory-side
+// atomics. The default absorb defers the new ids to its compress (newbits) and stores nothing here.
 // Anything else takes the full union.
 __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict__ parent, const char* __restrict__ msgs,
                                                                  u64 stride, u32 count, u32 skip, u32 n,
@@ -1521,8 +1524,9 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict
                 const u64 sj = __shfl(so, j, 64);
                 const u32 v = (u32)((w0 + (u64)j) * 64 + lane);
                 if (((t >> lane) & 1ull) && v != R) {
-                    if (v > R && !((sj >> lane) & 1ull)) gcc::st(&parent[v], R);  // a new id: one plain store
-                    else gcc::absorb_join(parent, v, R);
+                    // a new id: one CAS (a plain store could land after msg_absorb_kernel's CASes: DESIGN §3)
+                    if (!(v > R && !((sj >> lane) & 1ull) && gcc::cas(&parent[v], UNSEEN, R) == UNSEEN))
+                        gcc::absorb_join(parent, v, R);
                 }
             }
             continue;
@@ -1548,8 +1552,8 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_bits_kernel(u32* __restrict
 #pragma unroll
             for (int k = 0; k < kU; ++k)
                 if (on[k]) {
-                    if (v[k] > R && pv[k] == UNSEEN) gcc::st(&parent[v[k]], R);  // a new id: one plain store
-                    else gcc::absorb_join(parent, v[k], R);
+                    if (!(v[k] > R && pv[k] == UNSEEN && gcc::cas(&parent[v[k]], UNSEEN, R) == UNSEEN))  // a new id: one CAS
+                        gcc::absorb_join(parent, v[k], R);
                 }
         }
     }
@@ -1744,12 +1748,12 @@ struct FoldTune {
     // incremental compress (compress_inc_kernel): plain folds record their mutations in a bloom filter when the
     // forest spans >= inc_min_ids ids and a batch is at most 1/inc_div of them (a short window of a big forest)
     bool refresh_labels = false;  // mid-fold refreshes: bitmap only (false) or a full compress (true)
-    // OFF by default (end of round 3): with it on, C3 in 1M-edge windows at the defaults ended its last window with
-    // the right seen / component counts and a wrong label digest (a label left at a hooked root) in one full GPU
-    // run (profiles/r3ai_gpu_tests_c3_w1M_stale_label.log), the symptom of round 2's unexplained failure. Until its
-    // mechanism is found every emission takes the full compress; tune incremental=1 opts in (its tests run with
-    // inc_check, which re-derives every incremental compress)
-    bool incremental = false;
+    // On again since round 4. Rounds 2-3's stale label (a label left at a root hooked in the window, counts intact;
+    // profiles/r3ai_gpu_tests_c3_w1M_stale_label.log) was a PLAIN store of the recording fold's path splitting that
+    // reached memory after the in-place compress had rewritten the same slot (tools/stress_inc.py: 747 of 7854 C3/w1M
+    // streams at round 3's defaults; tools/probe_late_store.hip). The recording fold now writes parent[]
+    // with memory-side atomics only (inc_split = 0) and the blooms are cleared with atomics: 0 in the same stress
+    bool incremental = true;
     bool inc_inplace = true;  // the incremental compress rewrites only changed parent[] slots (no spare buffer)
     u64 inc_min_ids = 1ull << 22;
     // chosen by speed (round 3, tools/sweep_inc_div.py, profiles/r3c_sweep_inc_div.log): on C3 and C5 the recording
@@ -1763,9 +1767,13 @@ struct FoldTune {
     // diagnostics that leave the compress itself alone: a check kernel after every incremental compress (1), and the
     // previous labels kept for its records (2); gcc_forest_post_check_stats
     int post_check = 0;
-    // the recording fold (fold_kernel<true>): path splitting (plain stores) on / off, an agent release at its end
-    bool inc_split = true;
+    // the recording fold (fold_kernel<true>): path splitting (plain stores) on / off (OFF: the stale label above; no
+    // splitting is also faster on C3 / C5 windows: chains stay short between compresses), and fold_release: an agent
+    // release at the end of every block (1) or an s_waitcnt vmcnt(0) at the end of every wave (2) — A/B knobs of the
+    // mechanism (1 repairs the split fold, 2 does not: profiles/r4b_*)
+    bool inc_split = false;
     int fold_release = 0;
+    bool experimental = false;  // unlocks settings known to produce wrong results (inc_split = 1), for reproductions
     // bucketed fold of a fresh forest (bucket_fold.h): batches of >= bucket_min_batch edges over >= bucket_min_ids
     // ids (default: exactly the forests whose giant bitmap does not fit LDS); seeding = bucket_levels P2 + P3 levels
     // over the first bucket_sample of every bucket
@@ -1783,7 +1791,8 @@ struct FoldTune {
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
     int bucket_defer = 1;        // N labelled by the fold's closing compress instead of a store per id (bucket_join_kernel)
     int bucket_slow2 = 1;        // second filter level over the slow edges with C | N (C4's 1/8 share: 19 % slow edges)
-    int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms), 2 = 1024 x 12
+    int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms), 2 = 1024 x 12,
+                                 // 3 = 1024 x 16 with 8-entry write-out lanes (16-B hi stores)
     // FINAL P2 entries per thread per round: 8 or 12 (fewer barriers per entry; C4: P2 3.73 -> 3.23 ms,
     // profiles/r3c_ab_p2_per.log)
     int bucket_p2_per = 12;
@@ -2444,6 +2453,10 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
              : t.bucket_p1 == 1
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16>, dim3(h->n_cu), dim3(1024), bk::p1_lds(1024, 16),
                             edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err)
+             : t.bucket_p1 == 3
+                 ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16, 256, 8>, dim3(h->n_cu), dim3(1024),
+                            bk::p1_lds(1024, 16, 256, 8), edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap,
+                            h->d_err)
              : t.bucket_p1 == 2
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 12>, dim3(h->n_cu), dim3(1024), bk::p1_lds(1024, 12),
                             edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err)
@@ -2890,6 +2903,7 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::bucket_kernel<1024, 16>, (int)bk::p1_lds(1024, 16)},
         {(const void*)bk::bucket_kernel<1024, 12>, (int)bk::p1_lds(1024, 12)},
         {(const void*)bk::bucket_kernel<1024, 12, 512>, (int)bk::p1_lds(1024, 12, 512)},
+        {(const void*)bk::bucket_kernel<1024, 16, 256, 8>, (int)bk::p1_lds(1024, 16, 256, 8)},
     };
     for (const auto& t : tab) HIP_TRY(hipFuncSetAttribute(t.f, hipFuncAttributeMaxDynamicSharedMemorySize, t.bytes));
     return set_trace_slot();
@@ -3651,11 +3665,16 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "inc_min_ids") t.inc_min_ids = (u64)value;
     else if (k == "inc_div") t.inc_div = std::max<u64>(1, (u64)value);
     else if (k == "inc_check") t.inc_check = value != 0;
-    else if (k == "inc_split") t.inc_split = value != 0;
+    else if (k == "experimental") t.experimental = value != 0;
+    else if (k == "inc_split") {
+        if (value != 0 && !t.experimental)
+            return set_err(GCC_E_INVALID, "inc_split = 1 can produce wrong labels (DESIGN.md §3); set 'experimental' first");
+        t.inc_split = value != 0;
+    }
     else if (k == "fold_release") t.fold_release = (int)value;
     else if (k == "post_check") t.post_check = std::max(0, std::min(2, (int)value));
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
-    else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(2, (int)value));
+    else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
     else if (k == "bucket_defer") t.bucket_defer = value != 0.0;

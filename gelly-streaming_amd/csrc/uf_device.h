@@ -33,6 +33,9 @@ struct ReplayHooks {
     virtual void before(const u32* p) = 0;
     virtual u32 load(const u32* p, u32 fresh) = 0;
     virtual void wrote(const u32* p, u32 v) = 0;
+    // a PLAIN store (not an atomic): the model may let it land again later, after the next kernel's writes (round 4:
+    // a plain store of one kernel can become visible after stores of the next one)
+    virtual void stored(u32* p, u32 v) { (void)p, (void)v; }
 };
 inline ReplayHooks* replay = nullptr;  // null: plain relaxed atomics (product host code never sets it)
 #define UF_REPLAY_BEFORE(p) \
@@ -57,6 +60,7 @@ UF_HD void st(u32* p, u32 v) {
     UF_REPLAY_BEFORE(p);
     __atomic_store_n(p, v, __ATOMIC_RELAXED);
     UF_REPLAY_WROTE(p, v);
+    if (replay) replay->stored(p, v);
 #endif
 }
 UF_HD u32 cas(u32* p, u32 cmp, u32 val) {  // returns the old value (fresh: executed at the memory side)
@@ -253,6 +257,12 @@ struct UnionFind {
 
 typedef UnionFind<LoadPlain, true> UF;       // the fold's union (path splitting)
 typedef UnionFind<LoadPlain, false> UFRead;  // read-only finds (compress)
+// The RECORDING fold's union (fold_kernel<true>, before an incremental compress): no path splitting, so the fold writes
+// parent[] only with memory-side atomics. A plain store of a kernel can land after the next kernel's stores on gfx950
+// (round 4: tools/stress_inc.py, profiles/r4a_stress_*): a split store landing after the in-place compress rewrote its
+// slot put back a root hooked in that window (a wrong label, counts intact). With no plain store in the fold, every
+// value the compress writes stays written. (tests/cpp/test_uf_replay.cpp models such late stores.)
+typedef UnionFind<LoadPlain, false> UFRec;
 
 // ---- the per-id and per-edge steps of the other kernels, shared with the host replay ------------------------
 
@@ -275,11 +285,13 @@ UF_HD void unite_entry(u32* parent, u32 a, u32 b, u32 g) {
 }
 
 // msg_absorb_bits_kernel: an id x of a peer's giant, outside this forest's tracked component T (root R), joins R.
-// A new id above R by a PLAIN store — in that kernel x has no other writer — anything else by the union.
+// A new id above R by ONE CAS (UNSEEN -> R), anything else by the union. (Rounds 1-3 used a plain store — in that
+// kernel x has no other writer — but the next kernel, msg_absorb_kernel, may CAS the same slot, and a plain store can
+// land after the next kernel's memory-side atomics on gfx950: DESIGN.md §3.)
 UF_HD void absorb_join(u32* parent, u32 x, u32 R) {
     NoCount c;
-    if (x > R && ld(&parent[x]) == GCC_UNSEEN_DEV) st(&parent[x], R);
-    else UF::unite(parent, x, R, c);
+    if (x > R && ld(&parent[x]) == GCC_UNSEEN_DEV && cas(&parent[x], GCC_UNSEEN_DEV, R) == GCC_UNSEEN_DEV) return;
+    UF::unite(parent, x, R, c);
 }
 
 // compress_kernel's per-id step (out of place): labels[v] = root(v), UNSEEN stays UNSEEN.

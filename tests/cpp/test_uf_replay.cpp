@@ -7,7 +7,10 @@
 // returns, with probability stale/1000, an older value of the word from the history SINCE THE KERNEL STARTED
 // (its value at the kernel boundary, or any value stored or swapped in since) — what a load served from a CU's
 // non-coherent L1, or another XCD's L2, may return. Atomics (CAS, atomicMin, atomicOr) act on the fresh value,
-// as gfx950's memory-side atomics do. Kernel boundaries make everything visible (stream order: release/acquire).
+// as gfx950's memory-side atomics do. Kernel boundaries make atomics visible (stream order: release/acquire), but
+// NOT every plain store (round 4, measured on the MI355X: tools/stress_inc.py): with probability
+// late/1000 a plain store also LANDS AGAIN at a random point of the next kernel (controlled scheduler) or at its end
+// (free threads), overwriting whatever that kernel wrote to the word — a store still on its way when the kernel ended.
 //
 // Two schedulers:
 //   controlled ("ctl"): the threads run one memory operation at a time, the next thread chosen at random at every
@@ -19,13 +22,16 @@
 //   out            fold_kernel + compress_kernel (out of place: labels into the spare buffer)     [product]
 //   inplace_split  fold + a compress IN PLACE with path splitting (round 1's first compress)      [removed]
 //   inplace_nosplit fold + a compress in place, read-only finds                                  [experiment]
-//   inc            fold_kernel<REC> (bloom) + compress_inc_kernel<true> in place (inc_inplace)   [product]
+//   inc            fold_kernel<REC> (bloom, no path splitting: UFRec) + compress_inc_kernel<true> [product]
+//                  in place (inc_inplace)
+//   inc_split      the same with path splitting in the recording fold (round 3's product: the     [removed]
+//                  late split store over the in-place compress's root is the stale label)
 //   filter         fold_filtered_kernel's round: atomicMin hook + one-round-late settle + ring   [product]
 //                  entries (unite_entry), then the compress
 //   absorb         a peer's merge message: msg_absorb_bits_kernel (plain store of new ids) then  [product]
 //                  msg_absorb_kernel (lists), then the compress
 //
-// Input on stdin: V W then W window sizes, then the edges "u v". Args: pipeline mode threads seeds stale_pm.
+// Input on stdin: V W then W window sizes, then the edges "u v". Args: pipeline mode threads seeds stale_pm [late_pm].
 // Output: one line per seed with the failing windows, then "pipeline=<p> runs=<n> bad_runs=<k> bad_windows=<m>"
 // and, on the first failure, the id, its label, the expected label and the parent chain. With mode "labels" the
 // sequential reference labels of the last window are printed (one per line) for the oracle cross-check.
@@ -107,7 +113,18 @@ struct Sched {
 struct Model : gcc::ReplayHooks {
     bool controlled = false;
     unsigned stale_pm = 0;
+    unsigned late_pm = 0;
     Sched sched;
+    // late plain stores: issued in the current kernel (`late`), landing in the next one (`landing`, at op `at`)
+    struct Late {
+        u32* p;
+        u32 v;
+        u64 at;
+    };
+    std::mutex late_m;
+    std::vector<Late> late, landing;
+    u64 kernel_ops = 0;
+    u64 n_late = 0;
     // the tracked words: every parent[] array of the pipeline (loads elsewhere are never stale)
     std::vector<std::pair<u32*, u32>> arrays;
     std::vector<std::vector<std::vector<u32>>> hist;  // [array][id] -> values since the kernel start (ctl)
@@ -121,7 +138,16 @@ struct Model : gcc::ReplayHooks {
             }
         return false;
     }
+    void land(const Late& l) {
+        __atomic_store_n(l.p, l.v, __ATOMIC_RELAXED);
+        size_t a, i;
+        if (controlled && locate(l.p, a, i)) hist[a][i].push_back(l.v);
+    }
     void kernel_begin() {
+        landing.swap(late);
+        late.clear();
+        kernel_ops = 0;
+        for (auto& l : landing) l.at = controlled ? splitmix(sched.rng) % 4096 : ~0ull;
         hist.resize(arrays.size());
         start.resize(arrays.size());
         for (size_t a = 0; a < arrays.size(); ++a) {
@@ -136,7 +162,26 @@ struct Model : gcc::ReplayHooks {
         }
     }
     void before(const u32*) override {
-        if (controlled) sched.yield();
+        if (controlled) {
+            sched.yield();
+            ++kernel_ops;  // serialised by the scheduler
+            for (auto& l : landing)
+                if (l.at == kernel_ops) land(l);
+        }
+    }
+    void stored(u32* p, u32 v) override {
+        if (!late_pm || (splitmix(t_rng) % 1000) >= late_pm) return;
+        size_t a, i;
+        if (!locate(p, a, i)) return;
+        std::lock_guard<std::mutex> g(late_m);
+        late.push_back({p, v, 0});
+        ++n_late;
+    }
+    // the end of a kernel: the late stores of the previous kernel that have not landed yet land now
+    void kernel_end() {
+        for (auto& l : landing)
+            if (l.at > kernel_ops) land(l);
+        landing.clear();
     }
     u32 load(const u32* p, u32 fresh) override {
         if (!stale_pm || (splitmix(t_rng) % 1000) >= stale_pm) return fresh;
@@ -178,6 +223,12 @@ struct Model : gcc::ReplayHooks {
             sched.cv.notify_all();
         }
         for (auto& x : th) x.join();
+        kernel_end();
+    }
+    // host work between kernels that swaps or rereads arrays: whatever is still in flight lands first
+    void drain() {
+        kernel_begin();
+        kernel_end();
     }
 };
 
@@ -243,13 +294,15 @@ struct Forest {
     }
 };
 
-static void k_fold(Forest& f, const Edge* e, u64 n, int T, u64 seed, bool rec) {
+// rec: 0 plain fold; 1 the recording fold (UFRec: no path splitting, the product); 2 recording with path splitting
+static void k_fold(Forest& f, const Edge* e, u64 n, int T, u64 seed, int rec) {
     u32* par = f.parent.data();
     u32* bl = f.bloom[f.bloom_cur].data();
     g_model.kernel(T, seed, [&](int t) {
         gcc::NoCount c;
         for (u64 i = (u64)t; i < n; i += (u64)T) {
-            if (rec) gcc::UF::unite(par, e[i].a, e[i].b, c, gcc::BloomRec{bl});
+            if (rec == 1) gcc::UFRec::unite(par, e[i].a, e[i].b, c, gcc::BloomRec{bl});
+            else if (rec == 2) gcc::UF::unite(par, e[i].a, e[i].b, c, gcc::BloomRec{bl});
             else gcc::UF::unite(par, e[i].a, e[i].b, c);
         }
     });
@@ -421,6 +474,8 @@ static void chain_of(const std::vector<u32>& par, u32 v, std::vector<u32>& out) 
 
 static int run(const std::string& pipe, u32 V, const std::vector<u64>& wstart, const std::vector<Edge>& E, int T,
                u64 seed, std::vector<u32>& bad_windows, Failure& first) {
+    g_model.late.clear();  // late stores of an earlier run point into its freed forest
+    g_model.landing.clear();
     Forest f(V);
     SeqUF ref(V), peer(V);
     g_model.arrays = {{f.parent.data(), V}, {f.spare.data(), V}};
@@ -442,8 +497,8 @@ static int run(const std::string& pipe, u32 V, const std::vector<u64>& wstart, c
         } else if (pipe == "inplace_nosplit") {
             k_fold(f, e, n, T, ks + 1, false);
             k_compress_inplace<false>(f, T, ks + 2);
-        } else if (pipe == "inc") {
-            k_fold(f, e, n, T, ks + 1, true);
+        } else if (pipe == "inc" || pipe == "inc_split") {
+            k_fold(f, e, n, T, ks + 1, pipe == "inc" ? 1 : 2);
             compress_product_inc(f, T, ks + 2);
         } else if (pipe == "filter") {
             if (g == U) k_fold(f, e, n, T, ks + 1, false);  // the first window: nothing tracked yet
@@ -484,6 +539,7 @@ static int run(const std::string& pipe, u32 V, const std::vector<u64>& wstart, c
             std::fprintf(stderr, "unknown pipeline %s\n", pipe.c_str());
             std::exit(1);
         }
+        // the emission is read after the compress (the product's consumer reads after a synchronisation)
         const std::vector<u32> want = ref.labels();
         // after the compress parent[] IS the label array (out of place: swapped in; in place: rewritten)
         for (u32 v = 0; v < V; ++v)
@@ -519,6 +575,7 @@ int main(int argc, char** argv) {
     const int T = std::atoi(argv[3]);
     const int seeds = std::atoi(argv[4]);
     g_model.stale_pm = (unsigned)std::atoi(argv[5]);
+    g_model.late_pm = argc > 6 ? (unsigned)std::atoi(argv[6]) : 0;
     u32 V, W;
     if (std::scanf("%u %u", &V, &W) != 2) return 1;
     std::vector<u64> ws(W + 1, 0);
@@ -562,9 +619,10 @@ int main(int argc, char** argv) {
     }
     gcc::replay = nullptr;
     std::printf("pipeline=%s mode=%s threads=%d runs=%d bad_runs=%d bad_windows=%llu hooks=%llu hook_unions=%llu "
-                "absorb_stores=%llu inc_finds=%llu\n",
+                "absorb_stores=%llu inc_finds=%llu late_stores=%llu\n",
                 pipe.c_str(), mode.c_str(), T, seeds, bad_runs, (unsigned long long)bad_windows,
                 (unsigned long long)n_hooks.load(), (unsigned long long)n_hook_unions.load(),
-                (unsigned long long)n_absorb_stores.load(), (unsigned long long)n_inc_finds.load());
+                (unsigned long long)n_absorb_stores.load(), (unsigned long long)n_inc_finds.load(),
+                (unsigned long long)g_model.n_late);
     return 0;
 }

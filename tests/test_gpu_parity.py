@@ -556,7 +556,23 @@ KNOB_CASES = {
     "lds_edges_per_word": {"lds_edges_per_word": 1e9},  # the short windows take the global-bitmap filter
     "bucket_p2_per": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 12},
     "inc_check": {"incremental": 1, "inc_min_ids": 1024, "inc_div": 1, "inc_check": 1},  # diagnostics: checks every incremental compress
+    "post_check": {"incremental": 1, "inc_min_ids": 1024, "post_check": 2},  # diagnostics after every incremental compress
+    "fold_release": {"incremental": 1, "inc_min_ids": 1024, "fold_release": 1},
+    # inc_split = 1 is refused without `experimental` (test_unsafe_setting_needs_experimental); its default here
+    "inc_split": {"incremental": 1, "inc_min_ids": 1024, "inc_split": 0},
+    "experimental": {"experimental": 1},
 }
+
+
+def test_unsafe_setting_needs_experimental():
+    """The one setting known to give wrong results (inc_split = 1: round 3's stale label) is refused unless
+    the caller sets `experimental` first: a Java or C caller cannot turn it on by accident."""
+    with DisjointSet(1 << 16) as ds:
+        with pytest.raises(GellyCCError, match="experimental"):
+            ds.tune(inc_split=1)
+        ds.tune(experimental=1)
+        ds.tune(inc_split=1)  # accepted now (reproductions only)
+        ds.tune(inc_split=0)
 
 
 def header_tuning_keys():

@@ -1,7 +1,10 @@
 """CPU: the CC forest's device code (gelly-streaming_amd/csrc/uf_device.h) replayed on host threads
 (tests/cpp/test_uf_replay.cpp) under a model of gfx950's in-kernel memory behaviour: every memory operation a
 scheduling point, plain loads answered by stale but historically valid values (any value the word held since the
-kernel started), atomics on the fresh value, kernel boundaries making everything visible.
+kernel started), atomics on the fresh value, kernel boundaries making atomics visible — and, since round 4, plain
+stores that may land AGAIN in the next kernel (late_pm), after that kernel's own writes: measured on the MI355X
+(tools/stress_inc.py: C3 in 1M-edge windows, 747 wrong windows in 7854 streams with the recording fold's path
+splitting, none without it).
 
 Each pipeline is the kernel sequence of one product path (gelly_cc.hip): the fold + out-of-place compress, the
 bloom-recording fold + in-place incremental compress (inc_inplace), the filtered fold's atomicMin hook with its
@@ -40,15 +43,16 @@ def stream_text(parts, V):
     return text + "\n".join(f"{int(a)} {int(b)}" for p in parts for a, b in p) + "\n"
 
 
-def run(exe, pipe, mode, threads, seeds, stale_pm, text):
+def run(exe, pipe, mode, threads, seeds, stale_pm, text, late_pm=0):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", TSAN_OPTIONS="halt_on_error=1")
-    p = subprocess.run([exe, pipe, mode, str(threads), str(seeds), str(stale_pm)], input=text, capture_output=True,
-                       text=True, env=env, timeout=600)
+    p = subprocess.run([exe, pipe, mode, str(threads), str(seeds), str(stale_pm), str(late_pm)], input=text,
+                       capture_output=True, text=True, env=env, timeout=600)
     assert p.returncode == 0, f"{pipe} {mode}: exit {p.returncode}\n{p.stderr[-3000:]}"
     assert "ThreadSanitizer" not in p.stderr and "AddressSanitizer" not in p.stderr, p.stderr[-3000:]
     last = p.stdout.strip().split("\n")[-1]
     kv = dict(x.split("=") for x in last.split())
-    run.counts = {k: int(v) for k, v in kv.items() if k in ("hooks", "hook_unions", "absorb_stores", "inc_finds")}
+    run.counts = {k: int(v) for k, v in kv.items()
+                  if k in ("hooks", "hook_unions", "absorb_stores", "inc_finds", "late_stores")}
     return int(kv["bad_runs"]), p.stdout
 
 
@@ -128,3 +132,23 @@ def test_free_threads(build, exe):
         assert bad == 0, f"{pipe}:\n{out}"
         if pipe in exercised:  # the path under test was taken (bloom-hit finds, hook re-unions, plain stores)
             assert run.counts[exercised[pipe]] > 0, out
+
+
+def test_late_plain_stores(build):
+    """Round 4's stale label, replayed: with plain stores that land late (after the next kernel's writes), the
+    recording fold WITH path splitting before the in-place incremental compress loses labels (a split store of a root
+    hooked later in the window lands over the root the compress wrote), and the product's recording fold (UFRec, no
+    plain stores) does not. Every product pipeline stays exact under late stores too: the out-of-place compress writes
+    the other buffer, the filtered fold and the absorb are followed by an out-of-place compress."""
+    V, parts = big_stream(3)
+    text = stream_text(parts, V)
+    bad, out = run(ASAN, "inc_split", "free", 8, 4, 50, text, late_pm=20)
+    assert bad > 0 and run.counts["late_stores"] > 0, out
+    for pipe in PRODUCT:
+        bad, out = run(ASAN, pipe, "free", 8, 3, 50, text, late_pm=20)
+        assert bad == 0 and run.counts["late_stores"] > 0, f"{pipe}:\n{out}"
+    for seed in (1, 2):
+        V2, parts2 = chain_stream(seed)
+        for pipe in PRODUCT:
+            bad, out = run(ASAN, pipe, "ctl", 3, 100, 100, stream_text(parts2, V2), late_pm=100)
+            assert bad == 0, f"{pipe} (stream seed {seed}):\n{out}"
