@@ -42,7 +42,8 @@ constexpr int kP2Block = 1024;
 // P2 entries per thread per round (tune bucket_p2_per: 8 or 12): a round of kP2Block * PER entries, and at most that
 // many v's in the round's LDS tile + up to 3 padding slots per v-list (kMaxVLists)
 constexpr u32 p2_round(int per) { return (u32)kP2Block * per; }
-constexpr u32 p2_tile(int per) { return p2_round(per) + 3 * 256; }  // (3 x kMaxVLists)
+// + up to VW - 1 padding slots per v-list (kMaxVLists): VW = entries per lane in the write-out (4, or 8 since round 4)
+constexpr u32 p2_tile(int per, int vw = 4) { return p2_round(per) + (u32)(vw - 1) * 256; }
 // id ranges up to 2^28 (larger: the unbucketed fold): at most 512 buckets (2^19-id source slices) and 256 v-lists
 // (2^20-id target slices). P1's per-bucket LDS state is sized per instantiation (P1 MAXB: 256 up to 2^27 ids, 512
 // beyond, with a smaller tile); P2 / P3 keep per-v-list state only
@@ -528,7 +529,7 @@ __device__ __forceinline__ void hook_g(u32* parent, u32 g, u32 v) {
 // SEG (second level, FINAL only): the items are the slow-list runs the FINAL pass recorded (`segs`, m->nseg of
 // them; `bk` = the slow array), C is then C | N, and its own slow edges go to `slow` (the bucket storage, free
 // by then). FINAL without SEG records those runs into `segs` (one per item with slow edges; null: none).
-template <bool FINAL, bool SEG = false, int PER = 8>
+template <bool FINAL, bool SEG = false, int PER = 8, int VW = 4>
 __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict__ parent, const u32* __restrict__ bk_lo,
                                                                 const u16* __restrict__ bk_hi, const u64* __restrict__ bk,
                                                                 const u32* __restrict__ bits, u32 nwords32, u32 ns,
@@ -541,9 +542,9 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     trace_start(FINAL ? kTrBkP2 : kTrBkP2Seed);
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     u32* s_bits = s_dyn;                                   // kSliceWords
-    u32* s_vt = s_dyn + kSliceWords;                       // p2_tile(PER): the round's targets + run padding
+    u32* s_vt = s_dyn + kSliceWords;                       // p2_tile(PER, VW): the round's targets + run padding
     // per v-list state, kMaxVLists entries each
-    u32* s_cnt2 = s_vt + p2_tile(PER);                     // 2 x (double-buffered counts)
+    u32* s_cnt2 = s_vt + p2_tile(PER, VW);                 // 2 x (double-buffered counts)
     u32* s_pc = s_cnt2 + 2 * kMaxVLists;                   // counts padded to 4
     u32* s_start = s_pc + kMaxVLists;
     u32* s_vcap = s_start + kMaxVLists;
@@ -730,10 +731,10 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             GCC_PH_MARK(phc, 2);  // slow-list stores
             __syncthreads();  // (1) counts of this round complete
             GCC_PH_MARK(phc, 3);
-            // runs padded to a multiple of 4 with UNSEEN (P3 skips it): a lane writes 4 targets per store
-            count_scan<kP2Block>(s_cnt, s_start, nvs, s_wsum);
+            // runs padded to a multiple of VW with UNSEEN (P3 skips it): a lane writes VW targets per store
+            count_scan<kP2Block, VW>(s_cnt, s_start, nvs, s_wsum);
             for (u32 s = threadIdx.x; s < nvs; s += kP2Block) {
-                const u32 pc = pad4(s_cnt[s]);
+                const u32 pc = padw<VW>(s_cnt[s]);
                 if (pc) reserve_run(runs, s, pc, &m->vl_cur[s], s_vcap[s]);
                 for (u32 j = s_cnt[s]; j < pc; ++j) s_vt[s_start[s] + j] = 0xFFFFFFFFu;
                 s_cnt2[(rb ^ 1) * kMaxVLists + s] = 0;  // the next round's buffer
@@ -746,24 +747,40 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             GCC_PH_MARK(phc, 5);
             __syncthreads();  // (3) tile in bucket order
             GCC_PH_MARK(phc, 6);
-            const u32 tot4 = (s_start[nvs - 1] + pad4(s_cnt[nvs - 1])) / 4;
-            for (u32 x4 = threadIdx.x; x4 < tot4; x4 += kP2Block) {
-                const u4 v = reinterpret_cast<const u4*>(s_vt)[x4];  // slot 4 x4 is never padding
-                const u32 s = v.x >> kVSliceBits;
-                const u32 off = run_pos(runs, s, 4 * x4 - s_start[s]);  // a multiple of 4: one chunk
-                if (off != 0xFFFFFFFFu) {  // 8-B lo / 4-B hi stores (bases: 16-entry multiples, off: 4)
-                    const u16x4 lo = {(u16)v.x, (u16)v.y, (u16)v.z, (u16)v.w};
-                    constexpr u32 kHm = (1u << (kVSliceBits - 16)) - 1;  // the local id's bits above 16
-                    const u32 hi = (v.x >> 16 & kHm) | (v.y == 0xFFFFFFFFu ? kPadV : (v.y >> 16 & kHm)) << 8 |
-                                   (v.z == 0xFFFFFFFFu ? kPadV : (v.z >> 16 & kHm)) << 16 |
-                                   (u32)(v.w == 0xFFFFFFFFu ? kPadV : (v.w >> 16 & kHm)) << 24;
-                    *reinterpret_cast<u16x4*>(vl.lo + s_vbase[s] + off) = lo;
-                    *reinterpret_cast<u32*>(vl.hi + s_vbase[s] + off) = hi;
+            const u32 totw = (s_start[nvs - 1] + padw<VW>(s_cnt[nvs - 1])) / VW;
+            constexpr u32 kHm = (1u << (kVSliceBits - 16)) - 1;  // the local id's bits above 16
+            auto hib = [](u32 x) { return x == 0xFFFFFFFFu ? (u32)kPadV : (x >> 16 & kHm); };
+            for (u32 xw = threadIdx.x; xw < totw; xw += kP2Block) {
+                u32 v[VW];
+#pragma unroll
+                for (int k = 0; k < VW / 4; ++k) {  // slot VW xw is never padding
+                    const u4 q4 = reinterpret_cast<const u4*>(s_vt)[(VW / 4) * xw + k];
+                    v[4 * k] = q4.x;
+                    v[4 * k + 1] = q4.y;
+                    v[4 * k + 2] = q4.z;
+                    v[4 * k + 3] = q4.w;
+                }
+                const u32 s = v[0] >> kVSliceBits;
+                const u32 off = run_pos(runs, s, VW * xw - s_start[s]);  // a multiple of VW: one chunk
+                if (off != 0xFFFFFFFFu) {  // bases: 16-entry multiples, off: VW
+                    if constexpr (VW == 8) {  // 16-B lo / 8-B hi stores
+                        typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+                        const u16x8 lo = {(u16)v[0], (u16)v[1], (u16)v[2], (u16)v[3],
+                                          (u16)v[4], (u16)v[5], (u16)v[6], (u16)v[7]};
+                        const u64 hi = (u64)(hib(v[0]) | hib(v[1]) << 8 | hib(v[2]) << 16 | hib(v[3]) << 24) |
+                                       (u64)(hib(v[4]) | hib(v[5]) << 8 | hib(v[6]) << 16 | hib(v[7]) << 24) << 32;
+                        *reinterpret_cast<u16x8*>(vl.lo + s_vbase[s] + off) = lo;
+                        *reinterpret_cast<u64*>(vl.hi + s_vbase[s] + off) = hi;
+                    } else {  // 8-B lo / 4-B hi stores
+                        const u16x4 lo = {(u16)v[0], (u16)v[1], (u16)v[2], (u16)v[3]};
+                        const u32 hi = hib(v[0]) | hib(v[1]) << 8 | hib(v[2]) << 16 | hib(v[3]) << 24;
+                        *reinterpret_cast<u16x4*>(vl.lo + s_vbase[s] + off) = lo;
+                        *reinterpret_cast<u32*>(vl.hi + s_vbase[s] + off) = hi;
+                    }
                 } else if (FINAL) {  // the v-list is full: (u in C, v) = union(g, v) now
-                    hook_g(parent, g, v.x);
-                    if (v.y != 0xFFFFFFFFu) hook_g(parent, g, v.y);
-                    if (v.z != 0xFFFFFFFFu) hook_g(parent, g, v.z);
-                    if (v.w != 0xFFFFFFFFu) hook_g(parent, g, v.w);
+#pragma unroll
+                    for (int k = 0; k < VW; ++k)
+                        if (v[k] != 0xFFFFFFFFu) hook_g(parent, g, v[k]);
                 }
             }
             rb ^= 1;  // the write-out above is done before anyone passes the next round's barrier (1)

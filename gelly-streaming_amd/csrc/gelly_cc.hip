@@ -1620,8 +1620,8 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
 
 #include "bucket_fold.h"
 
-static constexpr size_t slice_filter_lds(int per = 8) {  // bucket_fold.h slice_filter_kernel's dynamic LDS
-    return (bk::kSliceWords + bk::p2_tile(per) + 11 * bk::kMaxVLists) * sizeof(u32) + bk::kMaxVLists * sizeof(u64) +
+static constexpr size_t slice_filter_lds(int per = 8, int vw = 4) {  // bucket_fold.h slice_filter_kernel's dynamic LDS
+    return (bk::kSliceWords + bk::p2_tile(per, vw) + 11 * bk::kMaxVLists) * sizeof(u32) + bk::kMaxVLists * sizeof(u64) +
            (bk::kP2Block / 64) * kRing * sizeof(u64);
 }
 
@@ -1796,6 +1796,7 @@ struct FoldTune {
     // FINAL P2 entries per thread per round: 8 or 12 (fewer barriers per entry; C4: P2 3.73 -> 3.23 ms,
     // profiles/r3c_ab_p2_per.log)
     int bucket_p2_per = 12;
+    int bucket_p2_vw = 4;  // FINAL P2's write-out: v-list entries per lane (4: 8-B + 4-B stores; 8: 16-B + 8-B)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -2487,12 +2488,12 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                       dim3(kBlock), 0, h->d_parent, h->cap, (const u32*)bits, (const bk::Meta*)h->d_meta, giant);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, nvs * sizeof(u32), h->stream));
-#define GCC_P2_FINAL(PER)                                                                                          \
-    launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true, false, PER>, dim3(p2_blocks), dim3(bk::kP2Block),    \
-             slice_filter_lds(PER), h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,       \
+#define GCC_P2_FINAL(PER, VW)                                                                                      \
+    launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true, false, PER, VW>, dim3(p2_blocks), dim3(bk::kP2Block), \
+             slice_filter_lds(PER, VW), h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,   \
              (const u32*)bits, nw32, ns, h->d_meta, vl, cps, 65536u, slot++, h->tune.drain_at, 0u, (const u32*)giant, \
              h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr)
-    rc = t.bucket_p2_per == 12 ? GCC_P2_FINAL(12) : GCC_P2_FINAL(8);
+    rc = t.bucket_p2_per == 12 ? (t.bucket_p2_vw == 8 ? GCC_P2_FINAL(12, 8) : GCC_P2_FINAL(12, 4)) : GCC_P2_FINAL(8, 4);
 #undef GCC_P2_FINAL
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
@@ -2896,6 +2897,7 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::slice_filter_kernel<true>, (int)slice_filter_lds()},
         {(const void*)bk::slice_filter_kernel<true, true>, (int)slice_filter_lds()},
         {(const void*)bk::slice_filter_kernel<true, false, 12>, (int)slice_filter_lds(12)},
+        {(const void*)bk::slice_filter_kernel<true, false, 12, 8>, (int)slice_filter_lds(12, 8)},
         {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kVSliceWords * sizeof(u32))},
         {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kVSliceWords * sizeof(u32))},
         {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
@@ -3676,6 +3678,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
+    else if (k == "bucket_p2_vw") t.bucket_p2_vw = (int)value == 8 ? 8 : 4;
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
     else if (k == "bucket_defer") t.bucket_defer = value != 0.0;
     else if (k == "bucket") t.bucket = value != 0;

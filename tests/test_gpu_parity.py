@@ -549,12 +549,14 @@ KNOB_CASES = {
     "bucket_levels": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_levels": 1},
     "bucket_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_sample": 1.0},
     "pin_chunk": {"pin_chunk": 4096},
-    "bucket_p1": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 0},
+    "bucket_p1": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 0},
+                  {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 3}],
     "bucket_slow2": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_slow2": 0},
     "bucket_defer": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_defer": 0},
     "bucket_hub_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_hub_sample": 0.1},
     "lds_edges_per_word": {"lds_edges_per_word": 1e9},  # the short windows take the global-bitmap filter
-    "bucket_p2_per": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 12},
+    "bucket_p2_per": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 8},
+    "bucket_p2_vw": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_vw": 8},
     "inc_check": {"incremental": 1, "inc_min_ids": 1024, "inc_div": 1, "inc_check": 1},  # diagnostics: checks every incremental compress
     "post_check": {"incremental": 1, "inc_min_ids": 1024, "post_check": 2},  # diagnostics after every incremental compress
     "fold_release": {"incremental": 1, "inc_min_ids": 1024, "fold_release": 1},
@@ -604,8 +606,9 @@ def test_every_tuning_knob_is_bit_exact(torch_cuda):
     with DisjointSet(V) as ds:
         with pytest.raises(GellyCCError):
             ds.tune(no_such_knob=1)
-    for key, knobs in KNOB_CASES.items():
-        print("knob case", key, flush=True)  # names the case in the report if a launch faults asynchronously
+    cases = [(k, c) for k, v in KNOB_CASES.items() for c in (v if isinstance(v, list) else [v])]
+    for key, knobs in cases:
+        print("knob case", key, knobs, flush=True)  # names the case in the report if a launch faults asynchronously
         with DisjointSet(V) as ds:
             ds.tune(**knobs)
             for w in range(len(starts) - 1):

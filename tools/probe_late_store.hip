@@ -40,20 +40,29 @@ __device__ __forceinline__ u32 mix(u32 x) {
     x ^= x >> 16;
     return x;
 }
-// word k of the M written words: hashed over the buffer (SPARSE) or the first M words (LINES)
+// word k of the M written words: hashed over the buffer (SPARSE; bit 4 clear, so that word | 16 — 64 B away in the
+// same 128-B line — is never a written word) or the first M words (LINES)
 template <bool SPARSE>
 __device__ __forceinline__ u32 word_of(u32 k, u32 w, u32 salt) {
-    return SPARSE ? mix(k * 0x9E3779B9u + salt) % w : k;
+    return SPARSE ? (mix(k * 0x9E3779B9u + salt) % w) & ~16u : k;
 }
 
 __global__ void k_fill(u32* buf, u32 w, u32 v) {
     for (u32 i = blockIdx.x * kBlock + threadIdx.x; i < w; i += gridDim.x * kBlock) buf[i] = v;
 }
 
-template <bool SPARSE, bool RELEASE>
+// ATOMIC_AFTER: after its plain store, the thread issues a memory-side atomic on ANOTHER word of the same 128-B line
+// (an atomic drops the issuing XCD's L2 copy of the line: what becomes of the dirty bytes of the plain store?). The
+// fold does exactly this: path-splitting stores and hook CASes on neighbouring slots. The other word (x | 16: 64 B
+// away, same line) is never one of the M written words (word_of).
+template <bool SPARSE, bool RELEASE, bool ATOMIC_AFTER = false>
 __global__ void k_write(u32* buf, u32 w, u32 m, u32 salt, u32 a) {
     if (SPARSE) {
-        for (u32 k = blockIdx.x * kBlock + threadIdx.x; k < m; k += gridDim.x * kBlock) buf[word_of<true>(k, w, salt)] = a;
+        for (u32 k = blockIdx.x * kBlock + threadIdx.x; k < m; k += gridDim.x * kBlock) {
+            const u32 x = word_of<true>(k, w, salt);
+            buf[x] = a;
+            if (ATOMIC_AFTER) atomicAdd(&buf[x | 16u], 0x100000u);
+        }
     } else {
         typedef u32 u4 __attribute__((ext_vector_type(4)));
         const u4 q = {a, a, a, a};
@@ -94,7 +103,7 @@ __global__ void k_check(u32* buf, u32 w, u32 m, u32 salt, u32 a, unsigned long l
     if (bad) atomicAdd(clobbered, (unsigned long long)bad);
 }
 
-template <bool SPARSE, bool RELEASE>
+template <bool SPARSE, bool RELEASE, bool ATOMIC_AFTER = false>
 static void run(const char* name, u32* buf, u32 w, u32 m, int iters, unsigned long long* d_cnt) {
     unsigned long long inv = 0, clob = 0;
     int bad_iters = 0;
@@ -103,7 +112,7 @@ static void run(const char* name, u32* buf, u32 w, u32 m, int iters, unsigned lo
         CK(hipMemset(d_cnt, 0, 2 * sizeof(unsigned long long)));
         hipLaunchKernelGGL(k_fill, dim3(kGrid), dim3(kBlock), 0, 0, buf, w, 0u);
         CK(hipDeviceSynchronize());  // the fill is in memory before A starts
-        hipLaunchKernelGGL((k_write<SPARSE, RELEASE>), dim3(kGrid), dim3(kBlock), 0, 0, buf, w, m, salt, a);
+        hipLaunchKernelGGL((k_write<SPARSE, RELEASE, ATOMIC_AFTER>), dim3(kGrid), dim3(kBlock), 0, 0, buf, w, m, salt, a);
         hipLaunchKernelGGL((k_cas<SPARSE>), dim3(kGrid), dim3(kBlock), 0, 0, buf, w, m, salt, a, b, d_cnt);
         hipLaunchKernelGGL((k_check<SPARSE>), dim3(kGrid), dim3(kBlock), 0, 0, buf, w, m, salt, a, d_cnt + 1);
         CK(hipGetLastError());
@@ -131,5 +140,8 @@ int main(int argc, char** argv) {
     run<true, true>("sparse 4-B plain stores + release per block, 1M words", buf, W, 1u << 20, iters, d_cnt);
     run<false, false>("whole lines, 16-B plain stores, 16M words", buf, W, 1u << 24, iters, d_cnt);
     run<false, false>("whole lines, 16-B plain stores, 1M words", buf, W, 1u << 20, iters, d_cnt);
+    run<true, false, true>("sparse 4-B plain stores + an atomic on the same line, 64K", buf, W, 1u << 16, iters, d_cnt);
+    run<true, false, true>("sparse 4-B plain stores + an atomic on the same line, 1M", buf, W, 1u << 20, iters, d_cnt);
+    run<true, true, true>("... + release per block, 1M", buf, W, 1u << 20, iters, d_cnt);
     return 0;
 }
