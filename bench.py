@@ -240,6 +240,17 @@ def make_roofline(kstats, phases, spans, inst_steps, workload, timing_note, host
     prof = profile_record(workload, dominant, dom.get("units_avg", 0)) if dominant else None
     achieved = dom.get("achieved_gbs")
     traffic = prof["hbm_bytes_per_launch"] if prof else None
+    # the committed PMC record is only this kernel's traffic if the kernel still runs as it did then: its duration in
+    # the PMC run's trace pass must be within 15 % of the live one; otherwise traffic is withheld
+    stale = None
+    if prof is not None and dom.get("ms_avg"):
+        at = prof.get("kernel_ms_at_pmc")
+        if at is None:
+            stale = "the PMC record has no kernel duration to check against"
+        elif abs(at - dom["ms_avg"]) > 0.15 * at:
+            stale = f"kernel {dom['ms_avg']:.3f} ms live vs {at:.3f} ms in the PMC run"
+        if stale and at is not None:
+            traffic = None
     avg_fold_s = (sum(ms for ms, _ in spans) / len(spans) / 1e3) if spans else None
     avg_fold_edges = (sum(n for _, n in spans) / len(spans)) if spans else None
     pipeline_gbs = BYTES_PER_EDGE * avg_fold_edges / avg_fold_s / 1e9 if spans and avg_fold_s else None
@@ -249,7 +260,8 @@ def make_roofline(kstats, phases, spans, inst_steps, workload, timing_note, host
     return {
         "bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-        "traffic": traffic, "traffic_unit": "bytes per launch",
+        "traffic": traffic, "traffic_unit": "bytes per launch", "traffic_check": stale or ("duration matches the PMC run"
+                                                                                          if traffic else None),
         "traffic_source": (prof["source"] + (f"; L2 hit rate {prof['l2_hit_rate']:.2f}" if "l2_hit_rate" in prof else "")
                            + f"; {prof['file']}") if traffic else None,
         "kernel_ms_avg": dom.get("ms_avg"), "kernel_units_per_launch": int(dom.get("units_avg", 0)),

@@ -58,6 +58,16 @@ def main():
     skip = ("gen_kernel", "__amd_rocclr_copyBuffer")
     per_step = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in rec["all_kernels"].items()
                    if not any(x in k for x in skip)) / max(1.0, steps)
+    # the kernel's average duration in the run's kernel-trace pass (tools/pmc_passes.sh): bench.py compares it with
+    # the live duration and withholds `traffic` when the kernel changed since (the record would be stale)
+    import glob
+    import os
+    for st in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
+        rows = [r for r in csv.DictReader(open(st)) if ksub in r["Name"]]
+        if rows:
+            calls = sum(int(r["Calls"]) for r in rows)
+            rec["kernel_ms_at_pmc"] = sum(float(r["TotalDurationNs"]) for r in rows) / max(1, calls) / 1e6
+            break
     rec["pipeline_traffic_per_step"] = per_step
     rec["pipeline_algorithmic_per_step"] = 16.0 * edges
     rec["pipeline_traffic_ratio"] = per_step / (16.0 * edges)
