@@ -925,13 +925,15 @@ __global__ __launch_bounds__(kBlock) void bucket_hook_kernel(u32* __restrict__ p
 // hooked here (each may become the component's root). Every later pass of
 // the fold treats an edge with one end in C | N as the hook of its other end (slow, rest), so nothing unions an
 // id of N directly; only FINAL P2's in-kernel ring unions (a full slow region, m->ring_used) could have made one
-// seen, and then every seen id of N is hooked under g here.
+// seen, and then every seen id of N is hooked under g here. later (a later window, round 4): ids of N may be seen
+// already, members of other components: every seen id of N is hooked under g here, only the new ones are deferred.
 __global__ __launch_bounds__(kBlock) void bucket_join_kernel(u32* __restrict__ parent, u32* __restrict__ bits,
                                                              const u32* __restrict__ nbits, u32 nwords32,
-                                                             const u32* __restrict__ giant, const Meta* __restrict__ m) {
+                                                             const u32* __restrict__ giant, const Meta* __restrict__ m,
+                                                             u32 later) {
     trace_start(kTrBkHook);
     const u32 g = *giant;
-    const bool ring = m->ring_used != 0;
+    const bool ring = m->ring_used != 0 || later;
     for (u64 w = (u64)blockIdx.x * kBlock + threadIdx.x; w < nwords32; w += (u64)gridDim.x * kBlock) {
         u32 d = nbits[w];
         if (!d) continue;

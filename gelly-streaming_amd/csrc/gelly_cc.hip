@@ -1796,7 +1796,10 @@ struct FoldTune {
     // FINAL P2 entries per thread per round: 8 or 12 (fewer barriers per entry; C4: P2 3.73 -> 3.23 ms,
     // profiles/r3c_ab_p2_per.log)
     int bucket_p2_per = 12;
-    int bucket_p2_vw = 4;  // FINAL P2's write-out: v-list entries per lane (4: 8-B + 4-B stores; 8: 16-B + 8-B)
+    int bucket_p2_vw = 4;
+    // the bucketed fold also for a later window of a forest tracking a giant (C4 in 8 windows: every window after the
+    // first took the filtered fold over an 8 MiB global bitmap, 2.2 ms per 2^27 edges; round 4)
+    int bucket_windows = 1;  // FINAL P2's write-out: v-list entries per lane (4: 8-B + 4-B stores; 8: 16-B + 8-B)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -2347,9 +2350,12 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
 // The bucketed fold of a fresh forest (bucket_fold.h): when it applies, and the pipeline.
 static u32 bucket_slices(const gcc_forest* h) { return (u32)(((u64)h->cap + bk::kSliceIds - 1) / bk::kSliceIds); }
 
+// A fresh forest (seeded from a hub), or (round 4, tune bucket_windows) a later window of a forest that tracks a giant:
+// then C is the tracked component's bitmap from the last compress, and the seeding and the reset are skipped.
 static bool bucket_applies(const gcc_forest* h, const u32* d_pairs, u64 n) {
     const FoldTune& t = h->tune;
-    return t.bucket && h->pending_reset && h->filter_enabled() && (u64)h->cap >= t.bucket_min_ids &&
+    const bool later = !h->pending_reset && t.bucket_windows && h->has_giant && !h->filter_off && h->compressed;
+    return t.bucket && (h->pending_reset || later) && h->filter_enabled() && (u64)h->cap >= t.bucket_min_ids &&
            n >= std::max<u64>(t.bucket_min_batch, 2 * bk::kP1Tile) && n < (1ull << 31) &&
            bucket_slices(h) <= bk::kMaxBuckets &&
            ((reinterpret_cast<uintptr_t>(d_pairs) | reinterpret_cast<uintptr_t>(h->d_parent) |
@@ -2392,6 +2398,7 @@ static int ensure_msg_scratch(gcc_forest* h) {
 
 static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const FoldTune& t = h->tune;
+    const bool fresh = h->pending_reset;  // else: a later window, C = the tracked component (bucket_applies)
     h->rec_all = false;
     int rc = alloc_filter(h);
     if (rc) return rc;
@@ -2464,13 +2471,16 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                  : launch_k(h, "bucket", n, bk::bucket_kernel<512, 16>, dim3(p1_blocks), dim3(512), bk::p1_lds(512, 16),
                             edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err);
     if (rc) return rc;
-    // seeding: C := {hub}, then levels over the sample
-    HIP_TRY(hipMemsetAsync(bits, 0, (size_t)nw32 * sizeof(u32), h->stream));
-    rc = launch_k(h, "bucket_hub", 0, bk::bucket_hub_kernel, dim3(1), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32), edges,
-                  n, h->cap, bits, h->d_meta);
+    // seeding (a fresh forest): C := {hub}, then levels over the sample. A later window keeps C = the tracked
+    // component's bitmap and its root (the last compress wrote both), and parent[] as it is.
+    if (fresh) {
+        HIP_TRY(hipMemsetAsync(bits, 0, (size_t)nw32 * sizeof(u32), h->stream));
+        rc = launch_k(h, "bucket_hub", 0, bk::bucket_hub_kernel, dim3(1), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32),
+                      edges, n, h->cap, bits, h->d_meta);
+    }
     const u32 frac = (u32)std::max(0.0, std::min(65536.0, t.bucket_sample * 65536.0));
     const u64 sample_edges = (u64)((double)n * frac / 65536.0);
-    const int levels = std::max(0, std::min(6, t.bucket_levels));
+    const int levels = fresh ? std::max(0, std::min(6, t.bucket_levels)) : 0;
     for (int l = 0; l < levels && !rc; ++l) {
         HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, nvs * sizeof(u32), h->stream));
         rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
@@ -2483,7 +2493,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                           bits, nw32, nvs, h->d_meta, vl, cps_seed_v, slot++, h->cap, h->d_err);
     }
     // parent[] := C ? g : UNSEEN (the reset), then every bucketed edge, the overflow list, a spill
-    if (!rc)
+    if (!rc && fresh)
         rc = launch_k(h, "bucket_init", 0, bk::bucket_init_kernel, dim3(grid_for(((u64)h->cap + 3) / 4, kMaxGrid)),
                       dim3(kBlock), 0, h->d_parent, h->cap, (const u32*)bits, (const bk::Meta*)h->d_meta, giant);
     if (rc) return rc;
@@ -2501,7 +2511,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const bool defer = t.bucket_defer != 0;
     if (!rc)
         rc = defer ? launch_k(h, "bucket_join", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
-                              h->d_parent, bits, (const u32*)h->d_nbits, nw32, (const u32*)giant, (const bk::Meta*)h->d_meta)
+                              h->d_parent, bits, (const u32*)h->d_nbits, nw32, (const u32*)giant, (const bk::Meta*)h->d_meta,
+                              (u32)!fresh)
                    : launch_k(h, "bucket_hook", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
                               h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
     // Second level over the slow edges, now against C | N: a slow edge whose source joined N is a hook of its
@@ -2523,7 +2534,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         if (!rc)
             rc = defer ? launch_k(h, "bucket_join2", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock),
                                   0, h->d_parent, bits, (const u32*)h->d_nbits, nw32, (const u32*)giant,
-                                  (const bk::Meta*)h->d_meta)
+                                  (const bk::Meta*)h->d_meta, (u32)!fresh)
                        : launch_k(h, "bucket_hook2", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock),
                                   0, h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
         slow_list = reinterpret_cast<const u64*>(h->d_bk);
@@ -3679,6 +3690,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
     else if (k == "bucket_p2_vw") t.bucket_p2_vw = (int)value == 8 ? 8 : 4;
+    else if (k == "bucket_windows") t.bucket_windows = value != 0;
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
     else if (k == "bucket_defer") t.bucket_defer = value != 0.0;
     else if (k == "bucket") t.bucket = value != 0;
