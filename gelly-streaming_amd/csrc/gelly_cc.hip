@@ -1799,7 +1799,8 @@ struct FoldTune {
     int bucket_p2_vw = 4;
     // the bucketed fold also for a later window of a forest tracking a giant (C4 in 8 windows: every window after the
     // first took the filtered fold over an 8 MiB global bitmap, 2.2 ms per 2^27 edges; round 4)
-    int bucket_windows = 1;  // FINAL P2's write-out: v-list entries per lane (4: 8-B + 4-B stores; 8: 16-B + 8-B)
+    int bucket_windows = 1;
+    int bucket_items = 4;  // P2 / P3 work items per CU (each loads its slice's bitmap into LDS)  // FINAL P2's write-out: v-list entries per lane (4: 8-B + 4-B stores; 8: 16-B + 8-B)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -2430,7 +2431,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         HIP_TRY(hipMemsetAsync(h->d_nbits, 0, (size_t)nw32 * sizeof(u32), h->stream));
     }
     const u32 ovf_cap = (u32)std::min<u64>(h->ovf_cap, 0xFFFFFFF0ull);
-    const u32 items = 4 * (u32)h->n_cu;  // dequeue items per P2 / P3 launch (parts of the slices)
+    const u32 items = (u32)std::max(1, t.bucket_items) * (u32)h->n_cu;  // dequeue items per P2 / P3 launch (parts of the slices)
     const u32 cps = std::max<u32>(1, (items + ns - 1) / ns);
     // A block loads a part's 64 KiB bitmap slice into LDS per item: a pass over few edges (the seeding levels of a
     // small batch) takes fewer, longer parts, about 64K edges per part at least
@@ -3691,6 +3692,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
     else if (k == "bucket_p2_vw") t.bucket_p2_vw = (int)value == 8 ? 8 : 4;
     else if (k == "bucket_windows") t.bucket_windows = value != 0;
+    else if (k == "bucket_items") t.bucket_items = std::max(1, std::min(64, (int)value));
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
     else if (k == "bucket_defer") t.bucket_defer = value != 0.0;
     else if (k == "bucket") t.bucket = value != 0;
