@@ -18,6 +18,9 @@
 #endif
 
 #define GCC_UNSEEN_DEV 0xFFFFFFFFu
+#ifndef GCC_UNITE_OPT  // the optimistic first CAS of unite (A/B builds: -DGCC_UNITE_OPT=0)
+#define GCC_UNITE_OPT 1
+#endif
 
 namespace gcc {
 
@@ -195,6 +198,14 @@ struct UnionFind {
     // union (DisjointSet.union :97-123), min-id hooking with a CAS on the larger root.
     // An unseen endpoint v joining a component whose root r < v is made seen AND hung under r by ONE CAS
     // (UNSEEN -> r): the common case of a stream (a new vertex attaching to an existing component).
+    // Optimistic first CAS (round 4, GCC_UNITE_OPT): the endpoints' observed parents pu, pv are tried as if they were
+    // the roots — right after a compress they are — before any find: CAS(parent[hi], hi, lo) with {lo, hi} = {pu, pv}.
+    // It succeeds only if hi is a root at that moment; then hi roots one endpoint's tree and lo < hi lies in the
+    // other's (a root is its tree's minimum, so lo cannot be in hi's tree: no cycle), and hanging hi under lo is the
+    // union — lo need not be a root (the invariant parent < self holds, and lo was a root at some time of the window
+    // or at its start, which is all the bloom of the incremental compress needs). Likewise an unseen v hangs under
+    // pu < v directly. A failed CAS returns hi's fresh parent and the general path below goes on from there.
+    // Saves the dependent load of parent[pu] / parent[pv] per edge in the common case of short windows.
     template <class R = NoRec>
     static UF_HD void unite(u32* parent, u32 u, u32 v, C& c, const R& rec = R()) {
         u32 pu = L::ld(&parent[u]);
@@ -211,6 +222,28 @@ struct UnionFind {
             u32 t = u; u = v; v = t;
             t = pu; pu = pv; pv = t;
         }
+#if GCC_UNITE_OPT
+        if (pu != GCC_UNSEEN_DEV) {
+            if (pv != GCC_UNSEEN_DEV) {  // both seen: the observed parents as roots
+                const u32 lo = pu < pv ? pu : pv, hi = pu < pv ? pv : pu;
+                c.cas();
+                const u32 old = gcc::cas(&parent[hi], hi, lo);
+                if (old == hi) {
+                    rec.mark(hi);
+                    return;
+                }
+                c.cas_fail();
+                // hi was not a root: its fresh parent replaces it as that endpoint's observed parent
+                if (hi == pu) pu = old;
+                else pv = old;
+            } else if (pu < v) {  // v unseen: hang it under u's observed parent (a node of u's tree, below v)
+                c.cas();
+                const u32 o = gcc::cas(&parent[v], GCC_UNSEEN_DEV, pu);
+                if (o == GCC_UNSEEN_DEV) return;
+                pv = o;  // v became seen meanwhile
+            }
+        }
+#endif
         if (pu == GCC_UNSEEN_DEV) {  // both unseen: make the smaller one seen (a root unless raced)
             const u32 lo = u < v ? u : v, hi = u < v ? v : u;
             c.cas();
