@@ -18,7 +18,11 @@
 #endif
 
 #define GCC_UNSEEN_DEV 0xFFFFFFFFu
-#ifndef GCC_UNITE_OPT  // the optimistic first CAS of unite (A/B builds: -DGCC_UNITE_OPT=0)
+// The optimistic first CAS of unite: 1 = an unseen endpoint hangs under the other's observed parent (no find first:
+// the CAS it saves the load for is issued anyway); 2 = also two seen endpoints' observed parents hooked directly
+// (measured: C3 one window -2.6 %, but C5's windows +7 % in the fold — the CAS fails whenever an observed parent was
+// hooked earlier in the window, and a failed atomic costs more than the load it saves; profiles/r4g_ab_*). 0 = off.
+#ifndef GCC_UNITE_OPT
 #define GCC_UNITE_OPT 1
 #endif
 
@@ -198,14 +202,14 @@ struct UnionFind {
     // union (DisjointSet.union :97-123), min-id hooking with a CAS on the larger root.
     // An unseen endpoint v joining a component whose root r < v is made seen AND hung under r by ONE CAS
     // (UNSEEN -> r): the common case of a stream (a new vertex attaching to an existing component).
-    // Optimistic first CAS (round 4, GCC_UNITE_OPT): the endpoints' observed parents pu, pv are tried as if they were
-    // the roots — right after a compress they are — before any find: CAS(parent[hi], hi, lo) with {lo, hi} = {pu, pv}.
+    // Optimistic first CAS (round 4, GCC_UNITE_OPT >= 2): the endpoints' observed parents pu, pv are tried as if they
+    // were the roots — right after a compress they are — before any find: CAS(parent[hi], hi, lo), {lo, hi} = {pu, pv}.
     // It succeeds only if hi is a root at that moment; then hi roots one endpoint's tree and lo < hi lies in the
     // other's (a root is its tree's minimum, so lo cannot be in hi's tree: no cycle), and hanging hi under lo is the
     // union — lo need not be a root (the invariant parent < self holds, and lo was a root at some time of the window
     // or at its start, which is all the bloom of the incremental compress needs). Likewise an unseen v hangs under
-    // pu < v directly. A failed CAS returns hi's fresh parent and the general path below goes on from there.
-    // Saves the dependent load of parent[pu] / parent[pv] per edge in the common case of short windows.
+    // pu < v directly (GCC_UNITE_OPT >= 1). A failed CAS returns hi's fresh parent and the general path below goes on
+    // from there. Saves the dependent load of parent[pu] per edge.
     template <class R = NoRec>
     static UF_HD void unite(u32* parent, u32 u, u32 v, C& c, const R& rec = R()) {
         u32 pu = L::ld(&parent[u]);
@@ -224,7 +228,7 @@ struct UnionFind {
         }
 #if GCC_UNITE_OPT
         if (pu != GCC_UNSEEN_DEV) {
-            if (pv != GCC_UNSEEN_DEV) {  // both seen: the observed parents as roots
+            if (GCC_UNITE_OPT >= 2 && pv != GCC_UNSEEN_DEV) {  // both seen: the observed parents as roots
                 const u32 lo = pu < pv ? pu : pv, hi = pu < pv ? pv : pu;
                 c.cas();
                 const u32 old = gcc::cas(&parent[hi], hi, lo);
