@@ -18,12 +18,13 @@
 #endif
 
 #define GCC_UNSEEN_DEV 0xFFFFFFFFu
-// The optimistic first CAS of unite: 1 = an unseen endpoint hangs under the other's observed parent (no find first:
-// the CAS it saves the load for is issued anyway); 2 = also two seen endpoints' observed parents hooked directly
-// (measured: C3 one window -2.6 %, but C5's windows +7 % in the fold — the CAS fails whenever an observed parent was
-// hooked earlier in the window, and a failed atomic costs more than the load it saves; profiles/r4g_ab_*). 0 = off.
+// The optimistic first CAS of unite (round 4 experiment, OFF): 1 = an unseen endpoint hangs under the other's
+// observed parent (no find first); 2 = also two seen endpoints' observed parents hooked directly. Measured against 0
+// (profiles/r4g_ab_*, r4h_ab_*, interleaved builds on one box): level 2 C3 one window -2.6 %, C5's windows +7 % in the
+// fold (the CAS fails whenever an observed parent was hooked earlier in the window, and a failed atomic costs more
+// than the load it saves); level 1 C5 +6.6 %, C3 equal. So 0: the find runs first.
 #ifndef GCC_UNITE_OPT
-#define GCC_UNITE_OPT 1
+#define GCC_UNITE_OPT 0
 #endif
 
 namespace gcc {
