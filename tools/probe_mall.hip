@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 
 typedef uint32_t u32;
 typedef uint64_t u64;
@@ -72,7 +73,9 @@ int main(int argc, char** argv) {
     for (int withstream = 0; withstream < 2; ++withstream) {
         for (u64 mb : sizes_mb) {
             const u64 n = (mb << 20) / 16;
-            const u64 ns = withstream ? (mb << 20) / 16 : 0;  // as many unrelated streamed bytes as the buffer
+            // as many unrelated streamed bytes as the buffer, at most the `other` allocation (round 4: the 2 GiB case read
+            // past the 1 GiB buffer and faulted the GPU; the figures before it were recorded)
+            const u64 ns = withstream ? std::min<u64>((mb << 20) / 16, other_b / 16) : 0;
             float best_w = 1e9f, best_r = 1e9f;
             for (int it = 0; it < iters; ++it) {
                 hipLaunchKernelGGL(k_stream, dim3(kGrid), dim3(kBlock), 0, 0, (const u4*)other, other_b / 16, sink);  // cold start
