@@ -67,6 +67,7 @@ struct Meta {
     u32 gmin;                    // min C (seeding)
     u32 nseg;                    // FINAL P2: slow-list segments recorded (SlowSeg table)
     u32 ring_used;               // FINAL P2 united some slow edges itself (its region was full): see bucket_join_kernel
+    u32 chunk;                   // entries per chunk reservation (chunk_entries)
     u32 slow_cnt[kMaxP2Blocks];  // FINAL P2: slow edges (source not in C) each block listed in its own region
 };
 
@@ -173,27 +174,31 @@ constexpr u32 kSample = 1u << 16;
 constexpr u32 kSlack = 1u << 12;
 // Writers reserve space in a bucket / v-list a CHUNK at a time per (block, slice) — one global atomic per chunk,
 // not per tile — and mark the unused tail of their last chunk with UNSEEN at exit (readers skip UNSEEN entries).
-// Each list's capacity therefore carries one chunk per writing block of slack.
-#ifndef GCC_KCHUNK
-#define GCC_KCHUNK 1024
-#endif
-constexpr u32 kChunk = GCC_KCHUNK;
+// Each list's capacity therefore carries one chunk per writing block of slack, and so do the lists' reads: C4's
+// 1/8 share carried 21M tail entries of 1024-entry chunks over 128 x 256 (bucket, block) pairs. The chunk is chosen
+// per batch (Meta::chunk, host: chunk_entries): 1024 entries from 2^29 edges up, 512 below (round 4, A/B in
+// profiles/r4k_*: the share and C4's 2^27-edge windows gain, C4 in one batch loses with 512)
+constexpr u32 kMaxChunk = 4096;
+__host__ __device__ inline u32 chunk_entries(u64 n, u32 tuned) {
+    const u32 c = tuned ? tuned : (n >= (1ull << 29) ? 1024u : 512u);
+    return c < 64 ? 64u : c > kMaxChunk ? kMaxChunk : (c + 15) / 16 * 16;
+}
 
 
 // The entries `nl` lists of an n-edge batch can claim (each list's capacity rounded up to 16); `aligned`: the buckets'
 // capacities of a batch of >= 2^26 edges are also rounded up to kBkAlign (the v-lists' are not).
-__host__ __device__ inline u64 storage_edges(u64 n, u32 nl, u32 blocks, bool aligned) {
-    return n + n / 4 + (u64)nl * (kSlack + 64 + (u64)blocks * kChunk) + 64 + (aligned ? (u64)nl * kBkAlign : 0);
+__host__ __device__ inline u64 storage_edges(u64 n, u32 nl, u32 blocks, bool aligned, u32 chunk) {
+    return n + n / 4 + (u64)nl * (kSlack + 64 + (u64)blocks * chunk) + 64 + (aligned ? (u64)nl * kBkAlign : 0);
 }
 
-__device__ __forceinline__ u32 est_cap(u32 hits, u64 n, u64 n_smp, u32 blocks) {
+__device__ __forceinline__ u32 est_cap(u32 hits, u64 n, u64 n_smp, u32 blocks, u32 chunk) {
     const u64 est = (u64)hits * n / (n_smp ? n_smp : 1);
-    const u64 c = ((est + est / 4 + kSlack + (u64)blocks * kChunk) + 15) / 16 * 16;  // 16-entry multiples: aligned
+    const u64 c = ((est + est / 4 + kSlack + (u64)blocks * chunk) + 15) / 16 * 16;  // 16-entry multiples: aligned
     return (u32)(c < 0xFFFFFFF0ull ? c : 0xFFFFFFF0ull);
 }
 
 // Chunked reservation of this round's run of `c` entries of slice s by the block (one thread per slice): the rest
-// of the block's current chunk [cpos, cend) first, then (if needed) a new chunk of max(kChunk, rest) entries from
+// of the block's current chunk [cpos, cend) first, then (if needed) a new chunk of max(chunk, rest) entries from
 // the list's global cursor, clamped to the capacity. The run's first l1 entries go to p1.., the next l2 to p2..,
 // the remaining c - l1 - l2 (capacity exhausted) overflow. Positions are list-relative.
 struct Runs {
@@ -205,7 +210,7 @@ struct Runs {
     u32* l2;
 };
 
-__device__ __forceinline__ void reserve_run(const Runs& r, u32 s, u32 c, u32* cursor, u32 cap) {
+__device__ __forceinline__ void reserve_run(const Runs& r, u32 s, u32 c, u32* cursor, u32 cap, u32 chunk) {
     const u32 have = r.cend[s] - r.cpos[s];
     const u32 a = c < have ? c : have;
     r.p1[s] = r.cpos[s];
@@ -214,7 +219,7 @@ __device__ __forceinline__ void reserve_run(const Runs& r, u32 s, u32 c, u32* cu
     r.l2[s] = 0;
     if (c > a) {
         const u32 need = c - a;
-        const u32 size = ((need > kChunk ? need : kChunk) + 15) / 16 * 16;
+        const u32 size = ((need > chunk ? need : chunk) + 15) / 16 * 16;
         const u32 g = atomicAdd(cursor, size);
         const u32 end = g >= cap ? cap : ((u64)g + size > cap ? cap : g + size);
         const u32 beg = g < cap ? g : cap;
@@ -249,7 +254,8 @@ __device__ __forceinline__ void block_prefix(const u32* cap, u64* base, u32 ns, 
 }
 
 __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
-                                                              Meta* __restrict__ m, u32 bk_blocks, u32 vl_blocks) {
+                                                              Meta* __restrict__ m, u32 bk_blocks, u32 vl_blocks,
+                                                              u32 chunk) {
     trace_start(kTrBkLayout);
     __shared__ u32 s_cu[kMaxBuckets], s_cv[kMaxVLists];
     __shared__ u64 s_scan[1024];
@@ -283,11 +289,11 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     }
     __syncthreads();
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
-        m->bk_cap[s] = est_cap(s_cu[s], n, n_smp, bk_blocks);
+        m->bk_cap[s] = est_cap(s_cu[s], n, n_smp, bk_blocks, chunk);
         if (bk_aligned(n)) m->bk_cap[s] = (u32)((m->bk_cap[s] + kBkAlign - 1) / kBkAlign * kBkAlign);
         m->bk_cur[s] = 0;
         if (s < nvs) {
-            m->vl_cap[s] = est_cap(s_cv[s], n, n_smp, vl_blocks);
+            m->vl_cap[s] = est_cap(s_cv[s], n, n_smp, vl_blocks, chunk);
             m->vl_cur[s] = 0;
         }
     }
@@ -297,37 +303,38 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     if (threadIdx.x < 16) m->work[threadIdx.x] = 0;
     if (threadIdx.x == 0) m->nseg = 0;
     if (threadIdx.x == 0) m->ring_used = 0;
+    if (threadIdx.x == 0) m->chunk = chunk;
     if (threadIdx.x == 0) {
         m->ovf_cur = 0;
         m->spill = 0;
     }
 }
 
-// Block-wide exclusive scan of the counts cnt[0..ns), each rounded up to a multiple of 4 (pad4: the runs' padded
-// lengths), into start[] (BLOCK threads, ns <= kMaxBuckets). One barrier inside.
-__device__ __forceinline__ u32 pad4(u32 c) { return (c + 3) & ~3u; }
+// Runs are padded to a multiple of W entries (W = 4 or 8): padw.
 template <u32 W>
 __device__ __forceinline__ u32 padw(u32 c) { return (c + W - 1) & ~(W - 1); }
-template <int BLOCK, u32 W = 4>
-__device__ __forceinline__ void count_scan(const u32* cnt, u32* start, u32 ns, u32* s_wsum) {
-    const u32 per = (ns + BLOCK - 1) / BLOCK;
+
+// Exclusive scan of the padded counts padw<W>(cnt[0..ns)) into start[], by wave 0 alone (lane l: lists
+// [l * per, l * per + per), per = ceil(ns / 64)), no barrier inside: the caller's next barrier publishes start[].
+// Round 4: the block-wide form (round 3) cost every round an extra barrier and, in wave w, w dependent LDS loads of
+// the other waves' sums, while only the first ns threads held counts.
+template <u32 W>
+__device__ __forceinline__ void wave_scan(const u32* cnt, u32* start, u32 ns) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 per = (ns + 63) >> 6;
     u32 loc = 0;
     for (u32 j = 0; j < per; ++j) {
-        const u32 s = threadIdx.x * per + j;
+        const u32 s = lane * per + j;
         loc += s < ns ? padw<W>(cnt[s]) : 0;
     }
-    const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     u32 inc = loc;
     for (int o = 1; o < 64; o <<= 1) {
         const u32 y = __shfl_up(inc, o, 64);
         if (lane >= (u32)o) inc += y;
     }
-    if (lane == 63) s_wsum[wv] = inc;
-    __syncthreads();
     u32 run = inc - loc;
-    for (u32 w = 0; w < wv; ++w) run += s_wsum[w];
     for (u32 j = 0; j < per; ++j) {
-        const u32 s = threadIdx.x * per + j;
+        const u32 s = lane * per + j;
         if (s < ns) {
             start[s] = run;
             run += padw<W>(cnt[s]);
@@ -360,17 +367,20 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
     // kernel's LDS beyond 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-bucket state below is static (MAXB >= ns)
     static_assert(MAXB <= kMaxBuckets, "Meta holds kMaxBuckets buckets");
     extern __shared__ __attribute__((aligned(16))) u64 s_srt[];
-    __shared__ u32 s_cnt[MAXB], s_start[MAXB], s_cap[MAXB];
+    // counts double-buffered by tile parity: a tile counts into one buffer while slower waves may still read the
+    // other (the previous tile's write-out); 3 barriers per tile (round 3: 6)
+    __shared__ u32 s_cntb[2 * MAXB], s_start[MAXB], s_cap[MAXB];
     __shared__ u32 s_cpos[MAXB], s_cend[MAXB], s_p1[MAXB], s_l1[MAXB], s_p2[MAXB], s_l2[MAXB];
     __shared__ u64 s_base[MAXB];
-    __shared__ u32 s_wsum[P1B / 64];
     const Runs runs{s_cpos, s_cend, s_p1, s_l1, s_p2, s_l2};
+    const u32 chunk = m->chunk;
     typedef u32 u4 __attribute__((ext_vector_type(4)));
     const u4* body = reinterpret_cast<const u4*>(edges);  // 16-B aligned (bucket_applies checks)
     for (u32 s = threadIdx.x; s < ns; s += P1B) {  // the layout, once per block (not a global load per edge)
         s_cap[s] = m->bk_cap[s];
         s_base[s] = m->bk_base[s];
         s_cpos[s] = s_cend[s] = 0;  // no chunk yet
+        s_cntb[s] = s_cntb[MAXB + s] = 0;
     }
     // Every thread reads every slice's state below — in the tile loop after its barriers, but a block with no
     // tile goes straight to the chunk-tail loop at the end. Without this barrier such a block read s_cpos / s_cend
@@ -400,8 +410,9 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
     if (t < ntiles) load_tile(t, q);
     [[maybe_unused]] PhaseClock phc;
     GCC_PH_START(phc);
+    u32 rb = 0;  // tile parity: the count buffer in use
     for (; t < ntiles; t += gridDim.x) {
-        for (u32 s = threadIdx.x; s < ns; s += P1B) s_cnt[s] = 0;
+        u32* s_cnt = s_cntb + rb * MAXB;
         u32 ua[P1P], va[P1P], rk[P1P];
         bool ok[P1P];
 #pragma unroll
@@ -415,31 +426,32 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
         }
         if (t + gridDim.x < ntiles) load_tile(t + gridDim.x, q);  // the next tile streams in meanwhile
         GCC_PH_MARK(phc, 0);  // waited for this tile's loads
-        __syncthreads();
-        GCC_PH_MARK(phc, 1);
 #pragma unroll
         for (int k = 0; k < P1P; ++k) {
             if (ok[k]) ok[k] = edge_ok(ua[k], va[k], cap, err);
             if (ok[k]) rk[k] = atomicAdd(&s_cnt[ua[k] >> kSliceBits], 1u);
         }
-        GCC_PH_MARK(phc, 2);  // LDS counting
-        __syncthreads();  // the tile's counts are complete
-        GCC_PH_MARK(phc, 3);
-        // every bucket's run is padded to a multiple of 4 with ~0 entries (P2 skips them), so that runs, tile
-        // slots and list positions stay multiples of 4 and the write-out moves 4 entries per lane (16 B of lo, 8 of hi)
-        count_scan<P1B, W>(s_cnt, s_start, ns, s_wsum);
+        GCC_PH_MARK(phc, 1);  // LDS counting
+        __syncthreads();  // (1) the tile's counts are complete; every wave has left the previous tile's write-out
+        GCC_PH_MARK(phc, 2);
+        // every bucket's run is padded to a multiple of W with ~0 entries (P2 skips them), so that runs, tile slots
+        // and list positions stay multiples of W and the write-out moves W entries per lane (4: 16 B of lo, 8 of hi)
+        if (threadIdx.x < 64) wave_scan<W>(s_cnt, s_start, ns);
+        for (u32 s = threadIdx.x; s < ns; s += P1B) s_cntb[(rb ^ 1) * MAXB + s] = 0;  // the next tile's buffer
+        GCC_PH_MARK(phc, 3);  // scan
+        __syncthreads();  // (2) starts
+        GCC_PH_MARK(phc, 4);
+        // the reservations (their global atomics) overlap the other waves' scatter
         for (u32 s = threadIdx.x; s < ns; s += P1B) {
             const u32 pc = padw<W>(s_cnt[s]);
-            if (pc) reserve_run(runs, s, pc, &m->bk_cur[s], s_cap[s]);
+            if (pc) reserve_run(runs, s, pc, &m->bk_cur[s], s_cap[s], chunk);
             for (u32 j = s_cnt[s]; j < pc; ++j) s_srt[s_start[s] + j] = ~0ull;
         }
-        __syncthreads();
-        GCC_PH_MARK(phc, 4);  // scan + reservations (+ barrier)
 #pragma unroll
         for (int k = 0; k < P1P; ++k)
             if (ok[k]) s_srt[s_start[ua[k] >> kSliceBits] + rk[k]] = ((u64)va[k] << 32) | ua[k];
-        GCC_PH_MARK(phc, 5);  // scatter
-        __syncthreads();
+        GCC_PH_MARK(phc, 5);  // reservations + scatter
+        __syncthreads();  // (3) the tile in bucket order, the runs reserved
         GCC_PH_MARK(phc, 6);
         const u32 totw = (s_start[ns - 1] + padw<W>(s_cnt[ns - 1])) / W;
         for (u32 xw = threadIdx.x; xw < totw; xw += P1B) {
@@ -477,8 +489,8 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
                 if (o + k > ovf_cap) m->spill = 1u;  // -> bucket_rest: the whole batch again
             }
         }
-        __syncthreads();
-        GCC_PH_MARK(phc, 7);  // write-out (+ barrier)
+        GCC_PH_MARK(phc, 7);  // write-out
+        rb ^= 1;  // the next tile's barrier (1) orders this write-out before its scan and scatter
     }
     GCC_PH_FLUSH(phc, 0);
     // the unused tails of this block's chunks: padding entries (P2 skips them)
@@ -545,13 +557,12 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     u32* s_vt = s_dyn + kSliceWords;                       // p2_tile(PER, VW): the round's targets + run padding
     // per v-list state, kMaxVLists entries each
     u32* s_cnt2 = s_vt + p2_tile(PER, VW);                 // 2 x (double-buffered counts)
-    u32* s_pc = s_cnt2 + 2 * kMaxVLists;                   // counts padded to 4
-    u32* s_start = s_pc + kMaxVLists;
+    u32* s_start = s_cnt2 + 2 * kMaxVLists;
     u32* s_vcap = s_start + kMaxVLists;
     u32* s_run = s_vcap + kMaxVLists;                      // 6 x: the chunk state (Runs)
     u64* s_vbase = reinterpret_cast<u64*>(s_run + 6 * kMaxVLists);
     u64* ring = s_vbase + kMaxVLists + (threadIdx.x >> 6) * kRing;  // FINAL only
-    __shared__ u32 s_item, s_wsum[kP2Block / 64], s_slow;
+    __shared__ u32 s_item, s_slow;
     typedef u32 u4 __attribute__((ext_vector_type(4)));
     constexpr int kQ = PER / 2;
     const u32 lane = threadIdx.x & 63;
@@ -561,6 +572,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
     u32 cur_slice = 0xFFFFFFFFu;
     u32 rb = 0;  // round parity: the counter buffer in use
     for (u32 s = threadIdx.x; s < 2 * kMaxVLists; s += kP2Block) s_cnt2[s] = 0;
+    const u32 chunk = m->chunk;
     const Runs runs{s_run, s_run + kMaxVLists, s_run + 2 * kMaxVLists, s_run + 3 * kMaxVLists,
                     s_run + 4 * kMaxVLists, s_run + 5 * kMaxVLists};
     const u32 nvs = vslices(cap);  // v-lists: target slices of 2^kVSliceBits ids
@@ -657,7 +669,9 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             GCC_PH_MARK(phc, 7);  // (previous round's write-out / item switch)
             u32* s_cnt = s_cnt2 + rb * kMaxVLists;
             u32 ua[PER], va[PER], rk[PER];
-            bool in[PER];
+            // per-entry flags as bit k of a VGPR (round 4: bool arrays became lane-mask SGPR pairs, 70 SGPRs
+            // spilled at PER = 12)
+            u32 in_m = 0;
             if constexpr (SEG) {
                 const bool skip_first = lo & 1, skip_last = hi & 1;  // the part starts / ends in the middle of a pair
 #pragma unroll
@@ -667,8 +681,8 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                     va[2 * k] = q[k].y;
                     ua[2 * k + 1] = q[k].z;
                     va[2 * k + 1] = q[k].w;
-                    in[2 * k] = j < np && !(skip_first && j == 0) && ua[2 * k] != 0xFFFFFFFFu;  // UNSEEN: a pad
-                    in[2 * k + 1] = j < np && !(skip_last && j == np - 1) && ua[2 * k + 1] != 0xFFFFFFFFu;
+                    in_m |= (u32)(j < np && !(skip_first && j == 0) && ua[2 * k] != 0xFFFFFFFFu) << (2 * k);  // UNSEEN: a pad
+                    in_m |= (u32)(j < np && !(skip_last && j == np - 1) && ua[2 * k + 1] != 0xFFFFFFFFu) << (2 * k + 1);
                 }
             } else {
 #pragma unroll
@@ -680,75 +694,97 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                     for (int c = 0; c < 4; ++c) {
                         const u16 h16 = (u16)(qh[k] >> (16 * c));
                         const bool real = bk_decode(lv[c], h16, sbase, ua[4 * k + c], va[4 * k + c]);
-                        in[4 * k + c] = j < np && real && e0 + c >= lo && e0 + c < hi;
+                        in_m |= (u32)(j < np && real && e0 + c >= lo && e0 + c < hi) << (4 * k + c);
                     }
                 }
             }
             u32 bad = 0;
 #pragma unroll
             for (int k = 0; k < PER; ++k) {  // the target indexes global lists (v-lists, parent[]): < cap
-                bad |= (u32)(in[k] && va[k] >= cap);
-                in[k] = in[k] && va[k] < cap;
+                const u32 big = (u32)(va[k] >= cap) & (in_m >> k);
+                bad |= big;
+                in_m &= ~(big << k);
             }
             if (bad) flag_err(err, kErrP2);
             GCC_PH_MARK(phc, 0);  // waited for this round's loads, decoded
             if (p0 + kRoundItems < np) load_round(p0 + kRoundItems);  // next round in flight
-            bool emit[PER];
-            u32 slow_m = 0;  // FINAL: this lane's slow edges (source not in C), bit k
+            u32 emit_m = 0;  // edges whose source is in C, bit k
 #pragma unroll
-            for (int k = 0; k < PER; ++k) {
-                const u32 iu = in[k] ? lds_bit(s_bits, ua[k] - sbase) : 0u;
-                emit[k] = in[k] && iu;
-                if (emit[k]) rk[k] = atomicAdd(&s_cnt[va[k] >> kVSliceBits], 1u);
-                slow_m |= (u32)(in[k] && !iu) << k;
-            }
-            GCC_PH_MARK(phc, 1);  // source lookups + LDS counting
-            if constexpr (FINAL) {  // the slow edges: into this block's region of the slow list, one LDS add per wave
-                const u32 ns_l = (u32)__popc(slow_m);
-                u32 incl = ns_l;
-                for (int o = 1; o < 64; o <<= 1) {
-                    const u32 y = __shfl_up(incl, o, 64);
-                    if (lane >= (u32)o) incl += y;
-                }
-                u32 base = 0;
-                if (lane == 63 && incl) base = atomicAdd(&s_slow, incl);
-                base = __shfl(base, 63, 64);
-                u32 pos = base + incl - ns_l, spill_m = 0;
+            for (int k = 0; k < PER; ++k)
+                if ((in_m >> k) & 1u) emit_m |= lds_bit(s_bits, ua[k] - sbase) << k;
+            if constexpr (SEG) {
+                // (round 4) the second level's other direction: an edge whose source is not in C | N but whose
+                // target is (the global bitmap: C | N, written by the join before this pass) hooks the SOURCE — it
+                // goes to the v-lists as u (P3 adds it to N', the join hooks it) instead of the slow list, where 3/4
+                // of C4's and the share's slow-kernel input were such hooks, profiles/r4j_stats_*.log)
+                u32 gw[PER];
+#pragma unroll
+                for (int k = 0; k < PER; ++k) gw[k] = ((in_m & ~emit_m) >> k) & 1u ? bits[va[k] >> 5] : 0u;
 #pragma unroll
                 for (int k = 0; k < PER; ++k)
-                    if ((slow_m >> k) & 1u) {
-                        if (pos < slow_cap) my_slow[pos] = ((u64)va[k] << 32) | ua[k];
-                        else spill_m |= 1u << k;
-                        ++pos;
+                    if ((gw[k] >> (va[k] & 31)) & 1u) {
+                        va[k] = ua[k];
+                        emit_m |= 1u << k;
                     }
-                if (__ballot(spill_m != 0)) {  // past the region (never at the default sizes): united right here
-                    if (lane == 0) atomicOr(&m->ring_used, 1u);
+            }
+            const u32 slow_m = in_m & ~emit_m;  // FINAL: this lane's slow edges (neither rule applies), bit k
 #pragma unroll
-                    for (int k = 0; k < PER; ++k)
-                        ring_push((spill_m >> k) & 1u, ua[k], va[k], ring, wq, wd, parent, drain_at, 0xFFFFFFFFu);
+            for (int k = 0; k < PER; ++k)
+                if ((emit_m >> k) & 1u) rk[k] = atomicAdd(&s_cnt[va[k] >> kVSliceBits], 1u);
+            GCC_PH_MARK(phc, 1);  // source lookups + LDS counting
+            if constexpr (FINAL) {  // the slow edges: into this block's region of the slow list, one LDS add per wave
+                // positions from one ballot per entry slot k (k-major: the lanes of one store are consecutive);
+                // round 3 scanned the lanes' counts with 6 cross-lane shuffles every round, slow edges or not
+                u32 tot = 0;
+#pragma unroll
+                for (int k = 0; k < PER; ++k) tot += (u32)__popcll(__ballot((slow_m >> k) & 1u));
+                if (tot) {  // wave-uniform
+                    u32 base = 0;
+                    if (lane == 0) base = atomicAdd(&s_slow, tot);
+                    base = __builtin_amdgcn_readfirstlane(base);
+                    u32 spill_m = 0;
+#pragma unroll
+                    for (int k = 0; k < PER; ++k) {
+                        const u64 b = __ballot((slow_m >> k) & 1u);
+                        if (b) {
+                            const u32 pos = base + __builtin_amdgcn_mbcnt_hi((u32)(b >> 32), __builtin_amdgcn_mbcnt_lo((u32)b, 0u));
+                            if ((slow_m >> k) & 1u) {
+                                if (pos < slow_cap) my_slow[pos] = ((u64)va[k] << 32) | ua[k];
+                                else spill_m |= 1u << k;
+                            }
+                            base += (u32)__popcll(b);
+                        }
+                    }
+                    if (__ballot(spill_m != 0)) {  // past the region (never at the default sizes): united right here
+                        if (lane == 0) atomicOr(&m->ring_used, 1u);
+#pragma unroll
+                        for (int k = 0; k < PER; ++k)
+                            ring_push((spill_m >> k) & 1u, ua[k], va[k], ring, wq, wd, parent, drain_at, 0xFFFFFFFFu);
+                    }
                 }
             }
             GCC_PH_MARK(phc, 2);  // slow-list stores
             __syncthreads();  // (1) counts of this round complete
             GCC_PH_MARK(phc, 3);
+            constexpr u32 kHm = (1u << (kVSliceBits - 16)) - 1;  // the local id's bits above 16
             // runs padded to a multiple of VW with UNSEEN (P3 skips it): a lane writes VW targets per store
-            count_scan<kP2Block, VW>(s_cnt, s_start, nvs, s_wsum);
+            if (threadIdx.x < 64) wave_scan<VW>(s_cnt, s_start, nvs);
+            for (u32 s = threadIdx.x; s < nvs; s += kP2Block) s_cnt2[(rb ^ 1) * kMaxVLists + s] = 0;  // next round's
+            __syncthreads();  // (2) starts
+            GCC_PH_MARK(phc, 4);
+            // the reservations (their global atomics) overlap the other waves' scatter
             for (u32 s = threadIdx.x; s < nvs; s += kP2Block) {
                 const u32 pc = padw<VW>(s_cnt[s]);
-                if (pc) reserve_run(runs, s, pc, &m->vl_cur[s], s_vcap[s]);
+                if (pc) reserve_run(runs, s, pc, &m->vl_cur[s], s_vcap[s], chunk);
                 for (u32 j = s_cnt[s]; j < pc; ++j) s_vt[s_start[s] + j] = 0xFFFFFFFFu;
-                s_cnt2[(rb ^ 1) * kMaxVLists + s] = 0;  // the next round's buffer
             }
-            __syncthreads();  // (2) starts + reservations
-            GCC_PH_MARK(phc, 4);
 #pragma unroll
             for (int k = 0; k < PER; ++k)
-                if (emit[k]) s_vt[s_start[va[k] >> kVSliceBits] + rk[k]] = va[k];
+                if ((emit_m >> k) & 1u) s_vt[s_start[va[k] >> kVSliceBits] + rk[k]] = va[k];
             GCC_PH_MARK(phc, 5);
             __syncthreads();  // (3) tile in bucket order
             GCC_PH_MARK(phc, 6);
             const u32 totw = (s_start[nvs - 1] + padw<VW>(s_cnt[nvs - 1])) / VW;
-            constexpr u32 kHm = (1u << (kVSliceBits - 16)) - 1;  // the local id's bits above 16
             auto hib = [](u32 x) { return x == 0xFFFFFFFFu ? (u32)kPadV : (x >> 16 & kHm); };
             for (u32 xw = threadIdx.x; xw < totw; xw += kP2Block) {
                 u32 v[VW];

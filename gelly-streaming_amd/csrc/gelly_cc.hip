@@ -1621,7 +1621,7 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
 #include "bucket_fold.h"
 
 static constexpr size_t slice_filter_lds(int per = 8, int vw = 4) {  // bucket_fold.h slice_filter_kernel's dynamic LDS
-    return (bk::kSliceWords + bk::p2_tile(per, vw) + 11 * bk::kMaxVLists) * sizeof(u32) + bk::kMaxVLists * sizeof(u64) +
+    return (bk::kSliceWords + bk::p2_tile(per, vw) + 10 * bk::kMaxVLists) * sizeof(u32) + bk::kMaxVLists * sizeof(u64) +
            (bk::kP2Block / 64) * kRing * sizeof(u64);
 }
 
@@ -1797,6 +1797,7 @@ struct FoldTune {
     // profiles/r3c_ab_p2_per.log)
     int bucket_p2_per = 12;
     int bucket_p2_vw = 4;
+    int bucket_chunk = 0;      // entries per chunk reservation in the bucketed fold's lists (0: by batch size)
     // the bucketed fold also for a later window of a forest tracking a giant (C4 in 8 windows: every window after the
     // first took the filtered fold over an 8 MiB global bitmap, 2.2 ms per 2^27 edges; round 4)
     int bucket_windows = 1;
@@ -2410,12 +2411,13 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     }
     const u32 p1_blocks = 2 * (u32)h->n_cu;  // (bucket_p1 = 1 runs n_cu blocks: fewer writers, same slack bound)
     const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
-    const u64 bk_S = bk::bk_entries(bk::storage_edges(n, ns, p1_blocks, bk::bk_aligned(n)));  // entries (a multiple of 2^19)
+    const u32 chunk = bk::chunk_entries(n, (u32)t.bucket_chunk);
+    const u64 bk_S = bk::bk_entries(bk::storage_edges(n, ns, p1_blocks, bk::bk_aligned(n), chunk));  // entries (a multiple of 2^19)
     if ((rc = grow(h->d_bk, h->bk_cap_bytes, bk::bk_bytes(bk_S), h->stream))) return rc;
     u32* bk_lo = reinterpret_cast<u32*>(h->d_bk);
     bk::u16* bk_hi = reinterpret_cast<bk::u16*>(h->d_bk + 4 * bk_S);
     if ((rc = grow(h->d_ovf, h->ovf_cap, n / 8 + 65536, h->stream))) return rc;
-    const u64 vl_S = bk::vl_entries(bk::storage_edges(n, bk::vslices(h->cap), p2_blocks, false));
+    const u64 vl_S = bk::vl_entries(bk::storage_edges(n, bk::vslices(h->cap), p2_blocks, false, chunk));
     if ((rc = grow(h->d_vl, h->vl_cap, bk::vl_bytes(vl_S), h->stream))) return rc;
     const bk::VList vl{reinterpret_cast<bk::u16*>(h->d_vl), h->d_vl + 2 * vl_S};
     // room for half the batch in the slow lists (C4: 3.9 % slow; C4's 1/8 share: more than the 12.5 % an n/8
@@ -2453,7 +2455,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const size_t vl_cur_off = offsetof(bk::Meta, vl_cur);
     u32 slot = 0;
     rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta,
-                  p1_blocks, p2_blocks);
+                  p1_blocks, p2_blocks, chunk);
     if (!rc)
         rc = ns > 256  // beyond 2^27 ids: 512 buckets' state and the 16K-edge tile exceed the LDS; 12K-edge tiles
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 12, 512>, dim3(h->n_cu), dim3(1024),
@@ -2504,8 +2506,20 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
              slice_filter_lds(PER, VW), h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,   \
              (const u32*)bits, nw32, ns, h->d_meta, vl, cps, 65536u, slot++, h->tune.drain_at, 0u, (const u32*)giant, \
              h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr)
-    rc = t.bucket_p2_per == 12 ? (t.bucket_p2_vw == 8 ? GCC_P2_FINAL(12, 8) : GCC_P2_FINAL(12, 4)) : GCC_P2_FINAL(8, 4);
+    rc = t.bucket_p2_per == 16   ? GCC_P2_FINAL(16, 4)
+         : t.bucket_p2_per == 12 ? (t.bucket_p2_vw == 8 ? GCC_P2_FINAL(12, 8) : GCC_P2_FINAL(12, 4))
+                                 : GCC_P2_FINAL(8, 4);
 #undef GCC_P2_FINAL
+    if (!rc && bucket_stats()) {  // diagnostics: FINAL P2's output (synchronises)
+        bk::Meta hm;
+        HIP_TRY(hipMemcpyAsync(&hm, h->d_meta, sizeof(hm), hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        u64 vl_used = 0, slow = 0;
+        for (u32 s = 0; s < nvs; ++s) vl_used += std::min(hm.vl_cur[s], hm.vl_cap[s]);
+        for (u32 b = 0; b < p2_blocks; ++b) slow += hm.slow_cnt[b];
+        std::fprintf(stderr, "[bucket] FINAL P2: v-list entries %llu, slow %llu (%.1f %%), slow runs %u\n",
+                     (unsigned long long)vl_used, (unsigned long long)slow, 100.0 * slow / n, hm.nseg);
+    }
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
                       h->d_nbits, nw32, nvs, h->d_meta, vl, cps_v, slot++, h->cap, h->d_err);
@@ -2517,7 +2531,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                    : launch_k(h, "bucket_hook", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
                               h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
     // Second level over the slow edges, now against C | N: a slow edge whose source joined N is a hook of its
-    // target (its v-list again), only the rest stays slow. Its input is FINAL P2's slow runs (one source slice
+    // target (its v-list again), one whose target is in C | N (the global bitmap) a hook of its source (round 4),
+    // only the rest stays slow. Its input is FINAL P2's slow runs (one source slice
     // each); its slow edges go to the bucket storage, which P2 has consumed.
     const u64* slow_list = h->d_slow;
     u32 slow_list_cap = slow_cap;
@@ -2567,12 +2582,31 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                      "(%.1f %%), overflow %u, spill %u, g=%u\n", (unsigned long long)n, ns,
                      (unsigned long long)bk_used, (unsigned long long)vl_used, 100.0 * vl_used / n,
                      (unsigned long long)slow, 100.0 * slow / n, hm.ovf_cur, hm.spill, hm.gmin);
+        // the slow kernel's input by kind, against the final C | N: both ends in it (nothing to do), one end (a hook
+        // of the other), neither (a union)
+        std::vector<u32> hb(nw32);
+        HIP_TRY(hipMemcpy(hb.data(), bits, (size_t)nw32 * sizeof(u32), hipMemcpyDeviceToHost));
+        u64 kinds[3] = {0, 0, 0};
+        std::vector<u64> seg;
+        for (u32 b = 0; b < p2_blocks; ++b) {
+            const u32 c = std::min(hm.slow_cnt[b], slow_list_cap);
+            seg.resize(c);
+            if (c) HIP_TRY(hipMemcpy(seg.data(), slow_list + (u64)b * slow_list_cap, (size_t)c * sizeof(u64), hipMemcpyDeviceToHost));
+            for (u64 e : seg) {
+                if (e == ~0ull) continue;
+                const u32 a = (u32)e, bb = (u32)(e >> 32);
+                const int ia = (hb[a >> 5] >> (a & 31)) & 1, ib = (hb[bb >> 5] >> (bb & 31)) & 1;
+                ++kinds[ia + ib == 2 ? 0 : ia + ib == 1 ? 1 : 2];
+            }
+        }
+        std::fprintf(stderr, "[bucket] slow kernel input vs C|N: both ends %llu, one end %llu, neither %llu\n",
+                     (unsigned long long)kinds[0], (unsigned long long)kinds[1], (unsigned long long)kinds[2]);
 #ifdef GCC_PHASES
         unsigned long long ph[2][16];
         HIP_TRY(hipMemcpyFromSymbol(ph, HIP_SYMBOL(bk::gcc_phase_acc), sizeof(ph)));
         static const char* const names[2][8] = {
-            {"loads", "barrier0", "count", "barrier1", "scan+reserve+barrier2", "scatter", "barrier3", "write-out+barrier4"},
-            {"loads+decode", "lookup+count", "slow stores", "barrier1", "scan+reserve+barrier2", "scatter", "barrier3",
+            {"loads", "count", "barrier1", "scan", "barrier2", "reserve+scatter", "barrier3", "write-out"},
+            {"loads+decode", "lookup+count", "slow stores", "barrier1", "scan+barrier2", "reserve+scatter", "barrier3",
              "write-out/item"}};
         for (int k = 0; k < 2; ++k) {
             unsigned long long tot = 0;
@@ -2910,6 +2944,7 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::slice_filter_kernel<true, true>, (int)slice_filter_lds()},
         {(const void*)bk::slice_filter_kernel<true, false, 12>, (int)slice_filter_lds(12)},
         {(const void*)bk::slice_filter_kernel<true, false, 12, 8>, (int)slice_filter_lds(12, 8)},
+        {(const void*)bk::slice_filter_kernel<true, false, 16, 4>, (int)slice_filter_lds(16, 4)},
         {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kVSliceWords * sizeof(u32))},
         {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kVSliceWords * sizeof(u32))},
         {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
@@ -3689,8 +3724,9 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "post_check") t.post_check = std::max(0, std::min(2, (int)value));
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
-    else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
+    else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 16 ? 16 : (int)value == 12 ? 12 : 8;
     else if (k == "bucket_p2_vw") t.bucket_p2_vw = (int)value == 8 ? 8 : 4;
+    else if (k == "bucket_chunk") t.bucket_chunk = std::max(0, std::min((int)bk::kMaxChunk, (int)value));
     else if (k == "bucket_windows") t.bucket_windows = value != 0;
     else if (k == "bucket_items") t.bucket_items = std::max(1, std::min(64, (int)value));
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
