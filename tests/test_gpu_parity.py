@@ -558,7 +558,6 @@ KNOB_CASES = {
     "bucket_p2_per": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 8},
                       {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 16}],
     "bucket_p2_vw": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_vw": 8},
-    "bucket_p2_direct": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_direct": 1},
     "bucket_chunk": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_chunk": 64},
                      {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_chunk": 4096}],
     "bucket_items": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_items": 1},
