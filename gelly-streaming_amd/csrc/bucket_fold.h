@@ -81,8 +81,9 @@ struct SlowSeg {
 
 __device__ __forceinline__ u32 lds_bit(const u32* s, u32 x) { return (s[x >> 5] >> (x & 31)) & 1u; }
 
-// Phase timing (diagnostic builds only: -DGCC_PHASES): thread 0 of every block accumulates clock64() deltas per
-// phase of P1's tile loop (kernel 0) and FINAL P2's round loop (kernel 1); GELLY_BUCKET_STATS prints them.
+// Phase timing (diagnostic builds only: -DGCC_PHASES): every wave accumulates clock64() deltas per phase of P1's tile
+// loop (kernel 0) and FINAL P2's round loop (kernel 1), summed over the owner waves (0-1) and the others apart;
+// GELLY_BUCKET_STATS prints them.
 #ifdef GCC_PHASES
 __device__ unsigned long long gcc_phase_acc[2][16];
 struct PhaseClock {
@@ -94,9 +95,9 @@ struct PhaseClock {
         acc[k] += n - t;
         t = n;
     }
-    __device__ __forceinline__ void flush(int kern) {
-        if (threadIdx.x == 0)
-            for (int k = 0; k < 8; ++k) atomicAdd(&gcc_phase_acc[kern][k], acc[k]);
+    __device__ __forceinline__ void flush(int kern) {  // lane 0 of every wave: waves 0-1 (the lists' owners) in
+        if ((threadIdx.x & 63) == 0)                     // slots 0-7, the other waves in slots 8-15
+            for (int k = 0; k < 8; ++k) atomicAdd(&gcc_phase_acc[kern][k + (threadIdx.x < 128 ? 0 : 8)], acc[k]);
     }
 };
 #define GCC_PH_START(pc) (pc).start()

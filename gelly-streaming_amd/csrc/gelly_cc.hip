@@ -2608,13 +2608,15 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
             {"loads", "count", "barrier1", "scan", "barrier2", "reserve+scatter", "barrier3", "write-out"},
             {"loads+decode", "lookup+count", "slow stores", "barrier1", "scan+barrier2", "reserve+scatter", "barrier3",
              "write-out/item"}};
-        for (int k = 0; k < 2; ++k) {
-            unsigned long long tot = 0;
-            for (int j = 0; j < 8; ++j) tot += ph[k][j];
-            std::fprintf(stderr, "[phases] %s:", k ? "P2" : "P1");
-            for (int j = 0; j < 8; ++j) std::fprintf(stderr, " %s %.1f%%", names[k][j], 100.0 * ph[k][j] / (tot ? tot : 1));
-            std::fprintf(stderr, " (total %.3g clk)\n", (double)tot);
-        }
+        for (int k = 0; k < 2; ++k)
+            for (int grp = 0; grp < 2; ++grp) {
+                unsigned long long tot = 0;
+                for (int j = 0; j < 8; ++j) tot += ph[k][8 * grp + j];
+                std::fprintf(stderr, "[phases] %s %s:", k ? "P2" : "P1", grp ? "other waves" : "waves 0-1");
+                for (int j = 0; j < 8; ++j)
+                    std::fprintf(stderr, " %s %.1f%%", names[k][j], 100.0 * ph[k][8 * grp + j] / (tot ? tot : 1));
+                std::fprintf(stderr, " (total %.3g clk)\n", (double)tot);
+            }
         unsigned long long zero[2][16] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(bk::gcc_phase_acc), zero, sizeof(zero)));
 #endif
