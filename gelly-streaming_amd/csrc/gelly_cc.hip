@@ -1950,6 +1950,16 @@ static bool bucket_stats() {
     return on;
 }
 
+// GELLY_BUCKET_ADDR=1 (diagnostics): every bucketed fold prints its buffers' device addresses (no synchronisation):
+// P1's time varies by up to 25 % between forests of one process (profiles/r4o_*), i.e. with where its buffers lie.
+static bool bucket_addr() {
+    static const bool on = [] {
+        const char* e = std::getenv("GELLY_BUCKET_ADDR");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
 // GELLY_SYNC_EACH=1 (diagnostics): synchronise after every launch, so that an asynchronous fault names its kernel.
 static bool sync_each_launch() {
     static const bool on = [] {
@@ -2415,6 +2425,10 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u64 bk_S = bk::bk_entries(bk::storage_edges(n, ns, p1_blocks, bk::bk_aligned(n), chunk));  // entries (a multiple of 2^19)
     if ((rc = grow(h->d_bk, h->bk_cap_bytes, bk::bk_bytes(bk_S), h->stream))) return rc;
     u32* bk_lo = reinterpret_cast<u32*>(h->d_bk);
+    if (bucket_addr())
+        std::fprintf(stderr, "[bucket-addr] edges %p bk %p (%llu entries) vl %p parent %p bits %p\n", (const void*)d_pairs,
+                     (const void*)h->d_bk, (unsigned long long)bk_S, (const void*)h->d_vl, (const void*)h->d_parent,
+                     (const void*)h->d_bits);
     bk::u16* bk_hi = reinterpret_cast<bk::u16*>(h->d_bk + 4 * bk_S);
     if ((rc = grow(h->d_ovf, h->ovf_cap, n / 8 + 65536, h->stream))) return rc;
     const u64 vl_S = bk::vl_entries(bk::storage_edges(n, bk::vslices(h->cap), p2_blocks, false, chunk));
