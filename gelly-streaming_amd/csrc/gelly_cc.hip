@@ -2520,9 +2520,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
              slice_filter_lds(PER, VW), h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,   \
              (const u32*)bits, nw32, ns, h->d_meta, vl, cps, 65536u, slot++, h->tune.drain_at, 0u, (const u32*)giant, \
              h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr)
-    rc = t.bucket_p2_per == 16   ? GCC_P2_FINAL(16, 4)
-         : t.bucket_p2_per == 12 ? (t.bucket_p2_vw == 8 ? GCC_P2_FINAL(12, 8) : GCC_P2_FINAL(12, 4))
-                                 : GCC_P2_FINAL(8, 4);
+    rc = t.bucket_p2_per == 12 ? (t.bucket_p2_vw == 8 ? GCC_P2_FINAL(12, 8) : GCC_P2_FINAL(12, 4)) : GCC_P2_FINAL(8, 4);
 #undef GCC_P2_FINAL
     if (!rc && bucket_stats()) {  // diagnostics: FINAL P2's output (synchronises)
         bk::Meta hm;
@@ -2960,7 +2958,6 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::slice_filter_kernel<true, true>, (int)slice_filter_lds()},
         {(const void*)bk::slice_filter_kernel<true, false, 12>, (int)slice_filter_lds(12)},
         {(const void*)bk::slice_filter_kernel<true, false, 12, 8>, (int)slice_filter_lds(12, 8)},
-        {(const void*)bk::slice_filter_kernel<true, false, 16, 4>, (int)slice_filter_lds(16, 4)},
         {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kVSliceWords * sizeof(u32))},
         {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kVSliceWords * sizeof(u32))},
         {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
@@ -3740,7 +3737,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "post_check") t.post_check = std::max(0, std::min(2, (int)value));
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
-    else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 16 ? 16 : (int)value == 12 ? 12 : 8;
+    else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
     else if (k == "bucket_p2_vw") t.bucket_p2_vw = (int)value == 8 ? 8 : 4;
     else if (k == "bucket_chunk") t.bucket_chunk = std::max(0, std::min((int)bk::kMaxChunk, (int)value));
     else if (k == "bucket_windows") t.bucket_windows = value != 0;

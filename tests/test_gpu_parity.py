@@ -555,8 +555,7 @@ KNOB_CASES = {
     "bucket_defer": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_defer": 0},
     "bucket_hub_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_hub_sample": 0.1},
     "lds_edges_per_word": {"lds_edges_per_word": 1e9},  # the short windows take the global-bitmap filter
-    "bucket_p2_per": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 8},
-                      {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 16}],
+    "bucket_p2_per": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 8},
     "bucket_p2_vw": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_vw": 8},
     "bucket_chunk": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_chunk": 64},
                      {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_chunk": 4096}],
