@@ -428,6 +428,103 @@ def windows_leg(name, ds_factory, windows, steps, warmup, digest, V, workload_ke
             "kernels_ms_per_step": {k: round(v["ms_per_step"], 5) for k, v in kstats.items()}}
 
 
+def bip_digests():
+    p = os.path.join(ROOT, "tests", "golden", "digests_bip.json")
+    return json.load(open(p)) if os.path.exists(p) else {}
+
+
+def bip_leg(ptr, E, V, steps, warmup, want, note, tune=None):
+    """BipartitenessCheck's summary (the signed forest, gcc_signed_*) at N = 1, edges already in HBM: per step reset +
+    fold + the emission on the device (compress). Timed bare on torch's stream, then fold and compress apart with
+    events; parity of the final words (digest, seen ids) and the success flag against tests/golden/digests_bip.json.
+    Roofline: the fold, priced like the CC plain fold (16 B per edge: the edge + both ends' words)."""
+    import torch
+
+    from gelly_stream import Candidates
+
+    c = Candidates(V).tune(**(tune or {}))
+    c.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    def step():
+        c.reset()
+        c.fold_device(ptr, E)
+        c.compress()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    fold_ms, comp_ms = [], []
+    for _ in range(max(1, min(steps, 3))):
+        c.reset()
+        ev[0].record()
+        c.fold_device(ptr, E)
+        ev[1].record()
+        c.compress()
+        ev[2].record()
+        torch.cuda.synchronize()
+        fold_ms.append(ev[0].elapsed_time(ev[1]))
+        comp_ms.append(ev[1].elapsed_time(ev[2]))
+    parity = None
+    if want is not None:
+        ok = c.getSuccess() == want["success"]
+        if ok and want["success"]:
+            w = c.words()
+            ok = str(label_digest(w)) == want["digest"] and int((w != 0xFFFFFFFF).sum()) == want["seen"]
+        parity = "bit-exact" if ok else "MISMATCH"
+    c.close()
+    fold_s = sorted(fold_ms)[len(fold_ms) // 2] / 1e3
+    achieved = 16 * E / fold_s / 1e9
+    return {"value": E / el, "unit": "edges/s", "ms_per_step": el * 1e3, "edges": E, "steps": steps, "parity": parity,
+            "success": want["success"] if want else None, "note": note,
+            "fold_ms": fold_s * 1e3, "compress_ms": sorted(comp_ms)[len(comp_ms) // 2],
+            "roofline": {"kernel": "signed_fold_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "bytes_per_unit": [16, "edge"],
+                         "timing": "torch events around the fold's launches on the forest's stream"}}
+
+
+def bip_legs(local, steps, warmup, d_edges=None, tune=None):
+    """BipartitenessCheck (VERDICT r3 missing 5): C3's and C4's per-rank share mapped bipartite
+    (generators.to_bipartite: every edge joins an even id to an odd one), and C3 as it is (an odd cycle early: the
+    fold stops once the summary has failed)."""
+    import torch
+
+    from gelly_stream import generators as G
+
+    digs = bip_digests()
+    out = {}
+    E3, V3 = G.CONFIGS["c3_gnm24"].info()
+    try:
+        d = torch.empty(2 * E3, dtype=torch.int32, device=f"cuda:{local}")
+        G.generate_device(G.CONFIGS["c3_gnm24"], 0, E3, d.data_ptr(), torch.cuda.current_stream(local).cuda_stream)
+        out["c3_gnm24"] = bip_leg(d.data_ptr(), E3, V3, steps, warmup, digs.get("c3_gnm24"),
+                                  "C3 as it is: not bipartite (an odd cycle once its giant forms)", tune)
+        G.to_bipartite_device(d)
+        out["bip_c3_gnm24"] = bip_leg(d.data_ptr(), E3, V3, steps, warmup, digs.get("bip_c3_gnm24"),
+                                      "to_bipartite(C3): 9.2M edges over 2^24 ids, one window", tune)
+        del d
+    except Exception as e:
+        out["bip_c3_gnm24"] = {"error": repr(e)}
+    if d_edges is not None:
+        try:
+            E4, V4 = G.CONFIGS["c4_kron26"].info()
+            share = 1 << 27
+            d = d_edges[: 2 * share].clone()
+            G.to_bipartite_device(d)
+            out["bip_c4_share"] = bip_leg(d.data_ptr(), share, V4, steps, warmup, digs.get("bip_c4_share"),
+                                          "to_bipartite(C4's first 2^27 edges): the kron hubs, one window", tune)
+            del d
+        except Exception as e:
+            out["bip_c4_share"] = {"error": repr(e)}
+    torch.cuda.empty_cache()
+    return out
+
+
 def config_legs(local, steps, warmup, digests, tune, d_edges=None):
     """Every other bench config of BASELINE.json at N = 1 beside the headline: C4's 1/8
     share (one rank's fold at N = 8), C4 in 8 windows (the windowed big-id-range path), C5 in 256 windows, C2 in 16
@@ -663,6 +760,11 @@ def main():
                                             d_edges if args.workload == "c4_kron26" else None)
         except Exception as e:
             result["configs"] = {"error": repr(e)}
+        try:
+            result["bipartiteness"] = bip_legs(local, args.steps, args.warmup,
+                                               d_edges if args.workload == "c4_kron26" else None)
+        except Exception as e:
+            result["bipartiteness"] = {"error": repr(e)}
         del d_edges
         torch.cuda.empty_cache()
         try:

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "abi_common.h"
@@ -48,9 +49,144 @@ __device__ __forceinline__ void sunite(u32* word, u32 u, u32 v, u32 q, u32* fail
 __global__ __launch_bounds__(256) void signed_fold_kernel(u32* __restrict__ word, const u64* __restrict__ edges, u64 n,
                                                          u32* __restrict__ fail) {
     const u64 stride = (u64)gridDim.x * 256;
-    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    u32 it = 0;
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride, ++it) {
+        // A failed summary is final: Candidates.merge answers fail() as soon as either side has failed (:78-81), so
+        // no later edge changes the emitted value (false, {}). Stop folding; a stale read only delays the exit.
+        // The words of a failed forest are not part of the contract (bipartite.py: getMap() == {}).
+        if ((it & 7) == 0 && suf::ld(fail)) return;
         const u64 e = __builtin_nontemporal_load(edges + i);
         sunite(word, (u32)e, (u32)(e >> 32), 1u, fail);
+    }
+}
+
+// ---- the giant-filtered fold (a skewed batch: kron / R-MAT hubs) ----
+// A plain fold of a hub-heavy batch contends on the hubs' roots (C4's 2^27-edge share: 24.7 ms, 5.3 G edges/s).
+// As the CC forest's filtered fold (gelly_cc.hip fold_filtered_kernel), most of such a batch lies inside one
+// component C: fold a prefix sample, vote C's root over sampled edges' roots, and snapshot per id two bits — in C,
+// and the parity to C's root (a find per seen id, as the compress; skipped, bits all 0, when no component holds
+// min_share of the samples: C3's random graph). Then an edge with both ends in
+// the snapshot's C is a pure check: the constraint sign(u) XOR sign(v) = 1 holds iff the parities differ (the
+// parity of a vertex to an ancestor is a fact, never changed by later writes), else the batch has an odd cycle
+// and the summary fails (Candidates.merge -> fail(), Candidates.java:77-139). It needs no forest access. Every
+// other edge takes the plain unite; an edge with one end in C also adds the other end to C (its parity from the
+// edge). A self loop inside C only adds its vertex: skipped.
+constexpr u32 kVoteSamples = 4096;
+constexpr u32 kVoteSlots = 8192;  // LDS hash of the sampled labels (a power of two)
+
+// one block: the most frequent root over kVoteSamples sampled edges' first ends of the folded prefix; vote[0] =
+// that root (or kUnseen), vote[1] = its count
+__global__ __launch_bounds__(1024) void signed_vote_kernel(u32* __restrict__ word, const u64* __restrict__ edges,
+                                                          u64 s, u32* __restrict__ vote) {
+    __shared__ u32 key[kVoteSlots], cnt[kVoteSlots];
+    __shared__ unsigned long long best;
+    for (u32 i = threadIdx.x; i < kVoteSlots; i += 1024) {
+        key[i] = kUnseen;
+        cnt[i] = 0;
+    }
+    if (threadIdx.x == 0) best = 0;
+    __syncthreads();
+    for (u32 k = threadIdx.x; k < kVoteSamples; k += 1024) {
+        const u64 e = edges[(u64)k * s / kVoteSamples];
+        const u32 w = suf::ld(&word[(u32)e]);
+        if (w == kUnseen) continue;
+        u32 par;
+        const u32 lab = sfind(word, (u32)e, w, par);
+        u32 h = (lab * 0x9E3779B1u) >> 19;  // 13 bits
+        while (true) {
+            const u32 o = atomicCAS(&key[h], kUnseen, lab);
+            if (o == kUnseen || o == lab) break;
+            h = (h + 1) & (kVoteSlots - 1);
+        }
+        atomicAdd(&cnt[h], 1u);
+    }
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < kVoteSlots; i += 1024)
+        if (cnt[i]) atomicMax(&best, ((unsigned long long)cnt[i] << 32) | key[i]);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        vote[0] = (u32)best;
+        vote[1] = (u32)(best >> 32);
+    }
+}
+
+// 2 bits per id, 16 ids per word: bit 2j = id 16w+j in the voted root's component, bit 2j+1 = its parity to the root.
+// No component when the vote's share is below 1/min_share_inv of the samples (a batch without a dominant one).
+__global__ __launch_bounds__(256) void signed_snapshot_kernel(u32* __restrict__ word, u32 n, const u32* __restrict__ vote,
+                                                             u32 min_count, u32* __restrict__ gbits) {
+    const bool on = vote[1] >= min_count;
+    const u32 r = vote[0];
+    const u32 nw = (n + 15) / 16;
+    for (u32 wi = blockIdx.x * 256 + threadIdx.x; wi < nw; wi += gridDim.x * 256) {
+        u32 b = 0;
+        if (on) {
+            for (u32 j = 0; j < 16; ++j) {
+                const u32 v = wi * 16 + j;
+                if (v >= n) break;
+                const u32 w = suf::ld(&word[v]);
+                if (w == kUnseen) continue;
+                u32 par = 0;
+                const u32 root = sw_parent(w) == v ? v : sfind(word, v, w, par);
+                if (root == r) b |= (1u | par << 1) << (2 * j);
+            }
+        }
+        gbits[wi] = b;
+    }
+}
+
+// one edge of the giant-filtered fold; bu / bv: the two ends' snapshot bits (bit 0 in C, bit 1 parity to r).
+// Returns whether the edge needs a unite.
+__device__ __forceinline__ bool giant_edge(u32* __restrict__ word, u32* __restrict__ gbits, u32* __restrict__ fail, u32 r,
+                                           u32 u, u32 v, u32 bu, u32 bv) {
+    if (bu & bv & 1u) {  // both in C: a check, no forest access
+        if (u != v && !((bu ^ bv) & 2u)) suf::st(fail, 1u);
+        return false;
+    }
+    if (!((bu ^ bv) & 1u)) return true;  // neither end in C
+    // one end in C: the other, x, joins C with the opposite parity (the edge's constraint); later edges on x are
+    // checks. Every bit is the parity the processed edges imply (snapshot: the forest's; derived: an edge that is
+    // united in the forest), so a check compares forest parities; two derivations that disagree are an
+    // odd cycle among forest edges, which the forest's unites report (fail), and a failed summary's bits no longer
+    // matter. A stale read of a bit only sends an edge to the unite.
+    const u32 x = (bu & 1u) ? v : u, px = (((bu & 1u) ? bu : bv) >> 1 & 1u) ^ 1u;
+    atomicOr(&gbits[x >> 4], (1u | px << 1) << (2 * (x & 15)));
+    // x unseen (its first edge: most of a kron batch's non-checks): hang it under r, C's root at the snapshot, an
+    // ancestor of every C member for good, with that parity — one CAS, no walks. Min-id hooking allows it when
+    // r < x; otherwise (or x seen) the unite.
+    return !(r < x && suf::ld(&word[x]) == kUnseen && suf::cas(&word[x], kUnseen, (r << 1) | px) == kUnseen);
+}
+
+// U edges per lane per step (i, i + stride, ...): their loads and bit lookups in flight together
+template <int U>
+__global__ __launch_bounds__(256) void signed_fold_giant_kernel(u32* __restrict__ word, const u64* __restrict__ edges, u64 n,
+                                                               u32* __restrict__ gbits, const u32* __restrict__ vote,
+                                                               u32* __restrict__ fail) {
+    const u32 r = vote[0];  // C's root at the snapshot (no bit is set when the vote found no C)
+    const u64 stride = (u64)gridDim.x * 256;
+    u32 it = 0;
+    for (u64 i0 = (u64)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += U * stride, ++it) {
+        if ((it & (U >= 8 ? 0 : 8 / U - 1)) == 0 && suf::ld(fail)) return;  // a failed summary is final
+        u64 e[U];
+        u32 bu[U], bv[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const u64 j = i0 + k * stride;
+            e[k] = __builtin_nontemporal_load(edges + (j < n ? j : n - 1));  // clamped: countable loads
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            bu[k] = gbits[(u32)e[k] >> 4];
+            bv[k] = gbits[(u32)(e[k] >> 32) >> 4];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const u32 u = (u32)e[k], v = (u32)(e[k] >> 32);
+            const bool want = i0 + k * stride < n &&
+                              giant_edge(word, gbits, fail, r, u, v, bu[k] >> (2 * (u & 15)), bv[k] >> (2 * (v & 15)));
+            // the unite inline: deferring them to a list and a second pass (per-block regions, wave-aggregated LDS
+            // appends) measured slower, 4.3 + 5.3 ms against 7.0 on C4's share (profiles/r4u_bip_*)
+            if (want) sunite(word, u, v, 1u, fail);
+        }
     }
 }
 
@@ -101,6 +237,11 @@ struct gcc_signed {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     bool compressed = true;
+    u32* d_gbits = nullptr;  // the giant-filtered fold's snapshot (2 bits per id) + 2 vote words
+    int giant = 1;           // gcc_signed_tune "giant": the giant-filtered fold for big batches
+    int sample_shift = 6;    // "sample_shift": its prefix sample = batch >> shift (at least 2^20 edges)
+    double min_share = 0.25; // "min_share": the voted component's share of the sampled edges, else the plain fold
+    int unroll = 1;          // "unroll": edges per lane per step of the giant-filtered fold (1, 2, 4, 8)
     std::vector<u32> host_words;
     bool host_valid = false;
 };
@@ -115,10 +256,41 @@ static int signed_compress(gcc_signed* h) {
     return GCC_OK;
 }
 
-// fold a device batch. The first launches are small and grow geometrically: while the hubs of a skewed stream
-// are still unhooked, few threads contend on their roots (the CC forest's sampled start, gelly_cc.hip).
+static int signed_fold_plain(gcc_signed* h, const u64* edges, u64 n);
+
+// a batch of at least 2^22 edges and a quarter of the id range (the snapshot's O(ids) passes amortised): the
+// giant-filtered fold (above signed_vote_kernel)
 static int signed_fold(gcc_signed* h, const u32* d_pairs, u64 n) {
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
+    if (!h->giant || n < (1ull << 22) || n < h->cap / 4) return signed_fold_plain(h, edges, n);
+    const u64 s = std::min<u64>(n, std::max<u64>(1ull << 20, n >> h->sample_shift));
+    int rc = signed_fold_plain(h, edges, s);
+    if (rc) return rc;
+    const u64 nw = ((u64)h->cap + 15) / 16;
+    if (!h->d_gbits) HIP_TRY(hipMalloc((void**)&h->d_gbits, (nw + 2) * sizeof(u32)));  // + the vote
+    u32* vote = h->d_gbits + nw;
+    hipLaunchKernelGGL(signed_vote_kernel, dim3(1), dim3(1024), 0, h->stream, h->d_word, edges, s, vote);
+    HIP_TRY(hipGetLastError());
+    const u32 min_count = (u32)std::max(1.0, h->min_share * kVoteSamples);
+    hipLaunchKernelGGL(signed_snapshot_kernel, dim3(grid_for_n(nw, kMaxGrid)), dim3(256), 0, h->stream, h->d_word, h->cap,
+                       vote, min_count, h->d_gbits);
+    HIP_TRY(hipGetLastError());
+    if (n > s) {
+        const dim3 g(grid_for_n(n - s, kMaxGrid));
+        auto k = h->unroll >= 8 ? signed_fold_giant_kernel<8>
+                 : h->unroll >= 4 ? signed_fold_giant_kernel<4>
+                 : h->unroll >= 2 ? signed_fold_giant_kernel<2> : signed_fold_giant_kernel<1>;
+        hipLaunchKernelGGL(k, g, dim3(256), 0, h->stream, h->d_word, edges + s, n - s, h->d_gbits, vote, h->d_fail);
+        HIP_TRY(hipGetLastError());
+    }
+    h->compressed = false;
+    h->host_valid = false;
+    return GCC_OK;
+}
+
+// the plain fold. The first launches are small and grow geometrically: while the hubs of a skewed stream are still
+// unhooked, few threads contend on their roots (the CC forest's sampled start, gelly_cc.hip).
+static int signed_fold_plain(gcc_signed* h, const u64* edges, u64 n) {
     u64 b = 0;
     for (u64 c = 4096; b < n; c *= 4) {
         const u64 e = std::min(n, b + c);
@@ -170,6 +342,7 @@ int gcc_signed_destroy(gcc_signed* h) {
     if (h->d_word) (void)hipFree(h->d_word);
     if (h->d_spare) (void)hipFree(h->d_spare);
     if (h->d_fail) (void)hipFree(h->d_fail);
+    if (h->d_gbits) (void)hipFree(h->d_gbits);
     if (h->d_stage) (void)hipFree(h->d_stage);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -251,6 +424,29 @@ int gcc_signed_merge(gcc_signed* into, gcc_signed* from) {
     into->compressed = false;
     into->host_valid = false;
     return GCC_OK;
+}
+
+int gcc_signed_tune(gcc_signed* h, const char* key, double value) {
+    CHECK_ARG(h && key, "null argument");
+    const std::string k(key);
+    if (k == "giant") h->giant = value != 0;
+    else if (k == "sample_shift") {
+        CHECK_ARG(value >= 0 && value <= 20, "sample_shift must be in [0, 20]");
+        h->sample_shift = (int)value;
+    } else if (k == "unroll") {
+        CHECK_ARG(value == 1 || value == 2 || value == 4 || value == 8, "unroll must be 1, 2, 4 or 8");
+        h->unroll = (int)value;
+    } else if (k == "min_share") {
+        CHECK_ARG(value > 0 && value <= 1, "min_share must be in (0, 1]");
+        h->min_share = value;
+    } else return gcc_set_err(GCC_E_INVALID, "gcc_signed_tune: unknown key '%s'", key);
+    return GCC_OK;
+}
+
+int gcc_signed_compress(gcc_signed* h) {
+    CHECK_ARG(h, "null handle");
+    DeviceGuard g(h->device);
+    return signed_compress(h);
 }
 
 int gcc_signed_words(gcc_signed* h, uint32_t* out, uint32_t n) {

@@ -151,6 +151,16 @@ class Candidates:
     def set_stream(self, hip_stream: Optional[int]) -> None:
         call("gcc_signed_set_stream", self.handle, c_void_p(hip_stream or 0), 1 if hip_stream is None else 0)
 
+    def tune(self, **knobs) -> "Candidates":
+        """Speed-only knobs of the signed fold (gcc_signed_tune): giant, sample_shift, min_share."""
+        for k, v in knobs.items():
+            call("gcc_signed_tune", self.handle, k.encode(), float(v))
+        return self
+
+    def compress(self) -> None:
+        """The emission on the device (canonical words in place; asynchronous): what words() copies out."""
+        call("gcc_signed_compress", self.handle)
+
     def words(self) -> np.ndarray:
         """Canonical words: (component min id << 1) | (sign differs from the minimum's), UNSEEN if unseen."""
         if self._words is None:

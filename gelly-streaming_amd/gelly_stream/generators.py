@@ -85,6 +85,23 @@ def generate_device(cfg: StreamConfig, first: int, count: int, d_pairs: int, hip
          ctypes.c_void_p(hip_stream))
 
 
+def to_bipartite(pairs: np.ndarray) -> np.ndarray:
+    """The bipartite version of a stream (BipartitenessCheck's bench legs): u -> u & ~1 (even ids, one side),
+    v -> v | 1 (odd ids, the other). Every edge joins the two sides, so the stream never fails; its components and
+    degrees keep the source's shape (a kron stream keeps its hubs). Ids stay below an even V."""
+    p = np.array(pairs, dtype=np.uint32, copy=True).reshape(-1, 2)
+    p[:, 0] &= np.uint32(0xFFFFFFFE)
+    p[:, 1] |= np.uint32(1)
+    return p
+
+
+def to_bipartite_device(t) -> None:
+    """to_bipartite in place on a device tensor of interleaved int32 pairs (torch; input preparation only)."""
+    v = t.view(-1, 2)
+    v[:, 0].bitwise_and_(-2)
+    v[:, 1].bitwise_or_(1)
+
+
 def timestamps(cfg: StreamConfig, first: int = 0, count: Optional[int] = None) -> np.ndarray:
     """Event timestamps (ms) of the stream; only the EXAMPLE stream carries the reference's timestamps."""
     n, _ = cfg.info()

@@ -187,6 +187,14 @@ int gcc_signed_fold_host(gcc_signed* h, const uint32_t* pairs, uint64_t n_edges)
 int gcc_signed_fold_device(gcc_signed* h, const uint32_t* d_pairs, uint64_t n_edges);
 /* combineFunction.reduce = Candidates.merge (BipartitenessCheck.java:128-130, Candidates.java:77-139) */
 int gcc_signed_merge(gcc_signed* into, gcc_signed* from);
+/* speed-only knobs (results identical): "giant" (1/0: the giant-filtered fold for batches of >= 2^22 edges and
+ * >= id_capacity / 4), "sample_shift" (its prefix sample = batch >> shift), "min_share" (the voted component's
+ * share of sampled edges below which the batch takes the plain fold), "unroll" (1/2/4/8 edges per lane per step of
+ * the giant-filtered fold). GCC_E_INVALID for an unknown key. */
+int gcc_signed_tune(gcc_signed* h, const char* key, double value);
+/* the emission on the device: the canonical words replace the forest (asynchronous on the forest's stream; what
+ * gcc_signed_words copies out). After a failure the words are unspecified (the emitted value is (false, {})). */
+int gcc_signed_compress(gcc_signed* h);
 int gcc_signed_words(gcc_signed* h, uint32_t* out, uint32_t n); /* canonical words of ids [0, n) */
 int gcc_signed_success(gcc_signed* h, int* success);              /* Candidates.getSuccess (:44-46) */
 

@@ -104,3 +104,30 @@ def test_reference_literal_divergence_is_pinned(path, golden):
         else:
             assert lit["success"] == x["success"]
     assert got == DIVERGENT.get(name, {}), (name, got)
+
+
+def test_to_bipartite_and_bench_digests(golden):
+    """generators.to_bipartite (bench.py's bip legs) makes every edge join an even id to an odd one, so the oracle
+    never fails on it; digests_bip.json's small-scale analogue: the same mapping of a scaled C3 folds to success and
+    its words digest is bench.label_digest's formula (make_bip_digests.words_digest)."""
+    import sys
+
+    from gelly_stream import generators as G
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_bip_digests as mk
+    from bench import label_digest
+
+    cfg = G.scaled(G.CONFIGS["c3_gnm24"], n_vertices=1 << 14, n_edges=1 << 15)
+    E, V = cfg.info()
+    raw = G.generate_host(cfg)
+    pairs = G.to_bipartite(raw)
+    assert np.all(pairs[:, 0] % 2 == 0) and np.all(pairs[:, 1] % 2 == 1) and pairs.max() < V
+    assert np.array_equal(raw, G.generate_host(cfg))  # a copy, not in place
+    r = orc.bip_stream(pairs, [0, E], V)
+    assert r["success"][0]
+    assert not orc.bip_stream(raw, [0, E], V)["success"][0]  # a random graph of this density has an odd cycle
+    assert mk.words_digest(r["words"][0]) == label_digest(r["words"][0])
+    fx = golden("digests_bip.json")
+    assert set(fx) == set(mk.ENTRIES)
+    assert fx["bip_c3_gnm24"]["success"] and fx["bip_c4_share"]["success"] and not fx["c3_gnm24"]["success"]

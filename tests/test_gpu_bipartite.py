@@ -132,3 +132,90 @@ def test_connected_components_tree_matches_bulk():
         assert np.array_equal(b.labels(), want[w]), w
         n += 1
     assert n == len(starts) - 1
+
+
+def test_bench_streams_full_size(golden):
+    """bench.py's bip legs at full size, device-resident: to_bipartite(C3) against the oracle's words digest
+    (tests/golden/digests_bip.json), and C3 as it is fails (the fold stops once failed; success stays false)."""
+    import torch
+
+    from bench import label_digest
+
+    want = golden("digests_bip.json")
+    cfg = G.CONFIGS["c3_gnm24"]
+    E, V = cfg.info()
+    d = torch.empty(2 * E, dtype=torch.int32, device="cuda:0")
+    G.generate_device(cfg, 0, E, d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    c = Candidates(V)
+    c.fold_device(d.data_ptr(), E)
+    assert c.getSuccess() == want["c3_gnm24"]["success"] is False
+    c.fold_device(d.data_ptr(), E)  # a failed summary stays failed
+    assert not c.getSuccess() and c.toString() == "(false,{})"
+    G.to_bipartite_device(d)
+    torch.cuda.synchronize()
+    c.reset()
+    c.fold_device(d.data_ptr(), E)
+    c.compress()
+    w = c.words()
+    assert c.getSuccess()
+    assert str(label_digest(w)) == want["bip_c3_gnm24"]["digest"]
+    assert int((w != UNSEEN).sum()) == want["bip_c3_gnm24"]["seen"]
+    c.close()
+
+
+@pytest.mark.parametrize("giant", [1, 0])
+@pytest.mark.parametrize("odd", [False, True])
+def test_kron_hubs_vs_oracle(odd, giant):
+    """A kron stream mapped bipartite (hubs: contended roots), 3 windows, every window's words vs the oracle. Window
+    1 (6M edges over 2^18 ids) takes the giant-filtered fold (gcc_signed_tune giant = 1, the default) or the plain
+    one (giant = 0); with one odd edge between two hubs' side the summary fails in that window (inside the giant:
+    the parity-bit check), and the next window's fold stops at once."""
+    import torch
+
+    cfg = G.scaled(G.CONFIGS["c4_kron26"], scale=18, n_edges=1 << 23)
+    E, V = cfg.info()
+    pairs = G.to_bipartite(G.generate_host(cfg))
+    if odd:
+        pairs[(3 * E) // 4] = [pairs[0, 0], pairs[1, 0]]  # two even ids: an even-even edge
+    starts = [0, 4096, (3 * E) // 4 + 1, E]
+    want = orc.bip_stream(pairs, starts, V, partitions=2)
+    assert want["success"][0] and (want["success"][1] != odd)  # the odd edge closes a cycle in window 1
+    d = torch.from_numpy(pairs.reshape(-1).view(np.int32)).cuda()
+    c = Candidates(V).tune(giant=giant)
+    for w in range(len(starts) - 1):
+        c.fold_device(d.data_ptr() + 8 * starts[w], starts[w + 1] - starts[w])
+        assert c.getSuccess() == bool(want["success"][w]), w
+        if want["success"][w]:
+            assert np.array_equal(c.words(), want["words"][w]), w
+    c.close()
+
+
+def test_giant_fold_knobs_and_no_dominant_component():
+    """The giant-filtered fold's knobs change speed only: to_bipartite(scaled C3) (no dominant component: the
+    snapshot stays empty) and a kron stream (a sample of 1/2 or 1/1024, min_share 1.0 = never filter) fold to the
+    same words as the plain fold; an unknown key is GCC_E_INVALID."""
+    import torch
+
+    from gelly_stream.native import GellyCCError
+
+    for cfg in (G.scaled(G.CONFIGS["c3_gnm24"], n_vertices=1 << 23, n_edges=1 << 22),
+                G.scaled(G.CONFIGS["c4_kron26"], scale=20, n_edges=1 << 22)):
+        E, V = cfg.info()
+        pairs = G.to_bipartite(G.generate_host(cfg))
+        d = torch.from_numpy(pairs.reshape(-1).view(np.int32)).cuda()
+        ref = Candidates(V).tune(giant=0)
+        ref.fold_device(d.data_ptr(), E)
+        want = ref.words().copy()
+        assert ref.getSuccess()
+        ref.close()
+        for knobs in ({}, {"sample_shift": 1}, {"sample_shift": 10}, {"min_share": 1.0}, {"min_share": 0.001},
+                      {"unroll": 1}, {"unroll": 8}):
+            c = Candidates(V).tune(**knobs)
+            c.fold_device(d.data_ptr(), E)
+            assert c.getSuccess() and np.array_equal(c.words(), want), (cfg.name, knobs)
+            c.close()
+    c = Candidates(16)
+    with pytest.raises(GellyCCError):
+        c.tune(no_such_knob=1)
+    c.close()
