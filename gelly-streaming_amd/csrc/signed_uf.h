@@ -75,13 +75,50 @@ SUF_HD u32 seen(u32* word, u32 v) {
 
 // the constraint sign(u) XOR sign(v) == q (an edge: q = 1; a merged (v, parent, parity) triple: q = parity).
 // A violated constraint inside one component sets *fail (an odd cycle: Candidates.merge -> fail()).
+// Both words are loaded before anything depends on them (round 4, as the CC forest's unite, uf_device.h):
+//   * both hang under the same parent p (a compressed forest, or one end is the other's parent): the constraint is
+//     a check of the two parities to p, no walk;
+//   * an unseen end v joining u's tree: ONE CAS hangs it under u's root ru with its parity (pu ^ q) when ru < v
+//     (min-id hooking), instead of a makeSet CAS and a hook CAS;
+//   * both unseen: the smaller becomes a root, the larger hangs under it.
+// A word read stale is one the slot held earlier: it points to an ancestor with the parity to it (facts), and
+// UNSEEN read stale is answered by the CAS's fresh value.
 SUF_HD void unite(u32* word, u32 u, u32 v, u32 q, u32* fail) {
-    u32 wu = seen(word, u);
-    if (u == v) return;  // a self loop only adds its vertex (edgeToCandidate ignores add()'s result)
-    u32 wv = seen(word, v);
+    u32 wu = ld(&word[u]);
+    if (u == v) {  // a self loop only adds its vertex (edgeToCandidate ignores add()'s result)
+        if (wu == kUnseen) (void)cas(&word[u], kUnseen, u << 1);
+        return;
+    }
+    u32 wv = ld(&word[v]);
+    if (wu != kUnseen && wv != kUnseen && parent_of(wu) == parent_of(wv)) {
+        if ((parity_of(wu) ^ parity_of(wv)) != q) st(fail, 1u);
+        return;
+    }
+    if (wu == kUnseen) {  // keep the unseen end (if any) in v
+        u32 t = u; u = v; v = t;
+        t = wu; wu = wv; wv = t;
+    }
+    if (wu == kUnseen) {  // both unseen: the smaller one seen (a root unless raced)
+        const u32 lo = u < v ? u : v, hi = u < v ? v : u;
+        const u32 o = cas(&word[lo], kUnseen, lo << 1);
+        u = lo;
+        wu = (o == kUnseen) ? (lo << 1) : o;
+        v = hi;
+    }
+    u32 pu, pv;
+    u32 ru = find(word, u, wu, pu);
+    if (wv == kUnseen) {
+        if (ru < v) {
+            const u32 o = cas(&word[v], kUnseen, (ru << 1) | (pu ^ q));
+            if (o == kUnseen) return;  // v seen and hung under ru in one step
+            wv = o;
+        } else {
+            const u32 o = cas(&word[v], kUnseen, v << 1);
+            wv = (o == kUnseen) ? (v << 1) : o;
+        }
+    }
     while (true) {
-        u32 pu, pv;
-        const u32 ru = find(word, u, wu, pu), rv = find(word, v, wv, pv);
+        const u32 rv = find(word, v, wv, pv);
         if (ru == rv) {
             if ((pu ^ pv) != q) st(fail, 1u);
             return;
@@ -92,6 +129,7 @@ SUF_HD void unite(u32* word, u32 u, u32 v, u32 q, u32* fail) {
         if (o == (hi << 1)) return;
         wu = seen(word, u);  // hi was hooked meanwhile: walk again; seen() answers a stale UNSEEN with the CAS's
         wv = seen(word, v);  // fresh value, so a stale line cannot spin this loop
+        ru = find(word, u, wu, pu);
     }
 }
 
