@@ -160,10 +160,18 @@ __device__ __forceinline__ bool giant_edge(u32* __restrict__ word, u32* __restri
 template <int U>
 __global__ __launch_bounds__(256) void signed_fold_giant_kernel(u32* __restrict__ word, const u64* __restrict__ edges, u64 n,
                                                                u32* __restrict__ gbits, const u32* __restrict__ vote,
-                                                               u32* __restrict__ fail) {
+                                                               u32 min_count, u32* __restrict__ fail) {
     const u32 r = vote[0];  // C's root at the snapshot (no bit is set when the vote found no C)
     const u64 stride = (u64)gridDim.x * 256;
     u32 it = 0;
+    if (vote[1] < min_count) {  // no C (the snapshot is empty): the plain fold, without the bit lookups
+        for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride, ++it) {
+            if ((it & 7) == 0 && suf::ld(fail)) return;
+            const u64 e = __builtin_nontemporal_load(edges + i);
+            sunite(word, (u32)e, (u32)(e >> 32), 1u, fail);
+        }
+        return;
+    }
     for (u64 i0 = (u64)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += U * stride, ++it) {
         if ((it & (U >= 8 ? 0 : 8 / U - 1)) == 0 && suf::ld(fail)) return;  // a failed summary is final
         u64 e[U];
@@ -280,7 +288,8 @@ static int signed_fold(gcc_signed* h, const u32* d_pairs, u64 n) {
         auto k = h->unroll >= 8 ? signed_fold_giant_kernel<8>
                  : h->unroll >= 4 ? signed_fold_giant_kernel<4>
                  : h->unroll >= 2 ? signed_fold_giant_kernel<2> : signed_fold_giant_kernel<1>;
-        hipLaunchKernelGGL(k, g, dim3(256), 0, h->stream, h->d_word, edges + s, n - s, h->d_gbits, vote, h->d_fail);
+        hipLaunchKernelGGL(k, g, dim3(256), 0, h->stream, h->d_word, edges + s, n - s, h->d_gbits, vote, min_count,
+                           h->d_fail);
         HIP_TRY(hipGetLastError());
     }
     h->compressed = false;
@@ -293,7 +302,9 @@ static int signed_fold(gcc_signed* h, const u32* d_pairs, u64 n) {
 static int signed_fold_plain(gcc_signed* h, const u64* edges, u64 n) {
     u64 b = 0;
     for (u64 c = 4096; b < n; c *= 4) {
-        const u64 e = std::min(n, b + c);
+        // past 2^20 edges the rest in one launch (to_bipartite(C3): 4M + 3.9M-edge tail launches 1.04 ms, one 8.2M
+        // launch after the 1M-edge prefix 0.92 ms, profiles/r4u_bip_r6r_*)
+        const u64 e = c >= (1ull << 20) ? n : std::min(n, b + c);
         hipLaunchKernelGGL(signed_fold_kernel, dim3(grid_for_n(e - b, kMaxGrid)), dim3(256), 0, h->stream, h->d_word,
                            edges + b, e - b, h->d_fail);
         HIP_TRY(hipGetLastError());
