@@ -460,6 +460,29 @@ int gcc_signed_compress(gcc_signed* h) {
     return signed_compress(h);
 }
 
+int gcc_signed_device_words(gcc_signed* h, const uint32_t** d_words) {
+    CHECK_ARG(h && d_words, "null argument");
+    *d_words = h->d_word;
+    return GCC_OK;
+}
+
+int gcc_signed_merge_words(gcc_signed* into, const uint32_t* d_words, uint32_t n, int other_failed) {
+    CHECK_ARG(into, "null handle");
+    CHECK_ARG(d_words || n == 0, "d_words is null");
+    CHECK_ARG(n <= into->cap, "n exceeds id_capacity");
+    DeviceGuard g(into->device);
+    if (other_failed) HIP_TRY(hipMemsetAsync(into->d_fail, 1, 1, into->stream));  // fail() is absorbing (:78-81)
+    if (n) {
+        // the other forest's (v, parent, parity) triples as constraints; its fail word is the flag above
+        hipLaunchKernelGGL(signed_merge_kernel, dim3(grid_for_n(n, kMaxGrid)), dim3(256), 0, into->stream, into->d_word,
+                           d_words, n, into->d_fail, into->d_fail);
+        HIP_TRY(hipGetLastError());
+    }
+    into->compressed = false;
+    into->host_valid = false;
+    return GCC_OK;
+}
+
 int gcc_signed_words(gcc_signed* h, uint32_t* out, uint32_t n) {
     CHECK_ARG(h, "null handle");
     CHECK_ARG(out || n == 0, "out is null");

@@ -157,6 +157,12 @@ class Candidates:
             call("gcc_signed_tune", self.handle, k.encode(), float(v))
         return self
 
+    def merge_words(self, d_words: int, n: int, other_failed: bool = False) -> "Candidates":
+        """self ∪= the signed partition in another forest's device words d_words[0, n) (gcc_signed_merge_words)."""
+        call("gcc_signed_merge_words", self.handle, c_void_p(d_words), int(n), 1 if other_failed else 0)
+        self._dirty()
+        return self
+
     def compress(self) -> None:
         """The emission on the device (canonical words in place; asynchronous): what words() copies out."""
         call("gcc_signed_compress", self.handle)
@@ -340,3 +346,38 @@ class BipartitenessCheck(SummaryBulkAggregation[Candidates, Candidates]):
                     n += batch.n
             if n:
                 yield summary
+
+
+def merge_group(c: Candidates, group=None) -> Candidates:
+    """combineFunction across ranks (BipartitenessCheck.java:128-130 over torch.distributed; gloo or RCCL): every
+    rank's ``c`` becomes the union of all ranks' summaries, failed if any rank's was. The words travel as one u32 per
+    id (all_gather; the compressed words are the partition's constraints), the fail flags by all_reduce(MAX); each
+    rank then merges its peers' words on its device (gcc_signed_merge_words). The merge is a union, so the order of
+    the peers does not matter and every rank ends with the same canonical words."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    failed = 0 if c.getSuccess() else 1
+    on_gpu = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+    flag = torch.tensor([failed], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if int(flag.item()):
+        c.merge_words(0, 0, other_failed=True)
+        return c
+    if world == 1:
+        return c
+    mine = torch.from_numpy(c.words().view(np.int32)).to(dev)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    for r, t in enumerate(parts):
+        if r == rank:
+            continue
+        d = t.to(torch.device("cuda", c.device)).contiguous()
+        torch.cuda.synchronize(c.device)  # the copy is on torch's stream; the merge on the forest's
+        c.merge_words(d.data_ptr(), c.id_capacity)
+        c.getSuccess()  # synchronises the forest's stream before d is freed
+    return c
+

@@ -125,6 +125,8 @@ _SIGS = {
     "gcc_signed_fold_device": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_signed_merge": (c_int, [c_void_p, c_void_p]),
     "gcc_signed_compress": (c_int, [c_void_p]),
+    "gcc_signed_merge_words": (c_int, [c_void_p, c_void_p, c_uint32, c_int]),
+    "gcc_signed_device_words": (c_int, [c_void_p, POINTER(c_void_p)]),
     "gcc_signed_tune": (c_int, [c_void_p, c_char_p, ctypes.c_double]),
     "gcc_signed_words": (c_int, [c_void_p, c_void_p, c_uint32]),
     "gcc_signed_success": (c_int, [c_void_p, POINTER(c_int)]),

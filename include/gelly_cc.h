@@ -187,6 +187,13 @@ int gcc_signed_fold_host(gcc_signed* h, const uint32_t* pairs, uint64_t n_edges)
 int gcc_signed_fold_device(gcc_signed* h, const uint32_t* d_pairs, uint64_t n_edges);
 /* combineFunction.reduce = Candidates.merge (BipartitenessCheck.java:128-130, Candidates.java:77-139) */
 int gcc_signed_merge(gcc_signed* into, gcc_signed* from);
+/* the same across processes (combineFunction over a transport; bipartite.merge_group): into ∪= the signed partition
+ * held in d_words[0, n) — another forest's words in device memory of into's device, compressed or not (a rank's
+ * gcc_signed_words / gcc_signed_device_words, sent); other_failed != 0: that summary had failed, so into fails.
+ * Asynchronous on into's stream: d_words must stay valid until that stream has run the merge. */
+int gcc_signed_merge_words(gcc_signed* into, const uint32_t* d_words, uint32_t n, int other_failed);
+/* the forest's own device words (valid until the next fold / compress / merge on h, which may swap buffers) */
+int gcc_signed_device_words(gcc_signed* h, const uint32_t** d_words);
 /* speed-only knobs (results identical): "giant" (1/0: the giant-filtered fold for batches of >= 2^22 edges and
  * >= id_capacity / 4), "sample_shift" (its prefix sample = batch >> shift), "min_share" (the voted component's
  * share of sampled edges below which the batch takes the plain fold), "unroll" (1/2/4/8 edges per lane per step of

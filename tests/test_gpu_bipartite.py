@@ -219,3 +219,83 @@ def test_giant_fold_knobs_and_no_dominant_component():
     with pytest.raises(GellyCCError):
         c.tune(no_such_knob=1)
     c.close()
+
+
+def _bip_group_worker(rank, world, port, pairs, starts, q):
+    """One rank (spawned before any GPU call): folds its contiguous 1/world of every window into a Candidates on
+    cuda:0, then bipartite.merge_group over gloo; reports (success, words) per window."""
+    import sys
+
+    root = os.path.dirname(HERE)
+    sys.path[:0] = [os.path.join(root, "gelly-streaming_amd")]
+    import torch
+    import torch.distributed as dist
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from gelly_stream.bipartite import Candidates as C
+        from gelly_stream.bipartite import merge_group
+
+        V = int(pairs.max()) + 1
+        d = torch.from_numpy(pairs.reshape(-1).view(np.int32)).cuda()
+        c = C(V)
+        out = []
+        for w in range(len(starts) - 1):
+            b, e = int(starts[w]), int(starts[w + 1])
+            lo, hi = b + (e - b) * rank // world, b + (e - b) * (rank + 1) // world
+            c.fold_device(d.data_ptr() + 8 * lo, hi - lo)
+            merge_group(c)
+            ok = c.getSuccess()
+            out.append((ok, c.words().copy() if ok else None))
+        dist.barrier()
+        q.put((rank, out))
+    except Exception as ex:
+        q.put((rank, repr(ex)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("odd", [False, True])
+def test_merge_group_two_ranks_share_one_gpu(odd):
+    """combineFunction across processes (bipartite.merge_group, gcc_signed_merge_words): 2 fresh ranks over gloo
+    each fold half of every window of a kron stream mapped bipartite; after each merge both hold the oracle's words
+    (the union of both halves); with an odd edge in rank 1's half of window 1, both ranks report the failure."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    cfg = G.scaled(G.CONFIGS["c4_kron26"], scale=16, n_edges=1 << 19)
+    E, V = cfg.info()
+    pairs = G.to_bipartite(G.generate_host(cfg))
+    pairs[-1] = [V - 2, V - 1]  # id V - 1 present, so every rank sizes its forest to V
+    starts = [0, 1000, E // 2, E]
+    if odd:
+        pairs[E // 2 - 10] = [pairs[0, 0], pairs[1, 0]]  # an even-even edge, in rank 1's half of window 1
+    want = orc.bip_stream(pairs, starts, V, partitions=2)
+    assert want["success"][0] and (want["success"][1] != odd)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bip_group_worker, args=(r, 2, port, pairs, starts, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        results = dict(q.get(timeout=150) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(2):
+        out = results[r]
+        assert isinstance(out, list), (r, out)
+        for w, (ok, words) in enumerate(out):
+            assert ok == bool(want["success"][w]), (r, w)
+            if ok:
+                assert np.array_equal(words, want["words"][w]), (r, w)
