@@ -1796,12 +1796,15 @@ struct FoldTune {
     // FINAL P2 entries per thread per round: 8 or 12 (fewer barriers per entry; C4: P2 3.73 -> 3.23 ms,
     // profiles/r3c_ab_p2_per.log)
     int bucket_p2_per = 12;
-    int bucket_p2_vw = 4;
+    int bucket_p2_vw = 4;      // FINAL P2's write-out: v-list entries per lane (4: 8-B + 4-B stores; 8: 16-B + 8-B)
     int bucket_chunk = 0;      // entries per chunk reservation in the bucketed fold's lists (0: by batch size)
     // the bucketed fold also for a later window of a forest tracking a giant (C4 in 8 windows: every window after the
     // first took the filtered fold over an 8 MiB global bitmap, 2.2 ms per 2^27 edges; round 4)
     int bucket_windows = 1;
-    int bucket_items = 4;  // P2 / P3 work items per CU (each loads its slice's bitmap into LDS)  // FINAL P2's write-out: v-list entries per lane (4: 8-B + 4-B stores; 8: 16-B + 8-B)
+    int bucket_items = 4;  // P2 / P3 work items per CU (each loads its slice's bitmap into LDS)
+    // tests only: the fail_absorb-th next gcc_forest_absorb_many call fails with GCC_E_INTERNAL before it launches
+    // anything (0: never) — a rank's absorb failing inside the cross-GPU group merge (tests/test_gpu_group.py)
+    int fail_absorb = 0;
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -3456,6 +3459,8 @@ int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_by
     CHECK_ARG(((reinterpret_cast<uintptr_t>(d_msgs) | stride_bytes) & 15) == 0, "messages must be 16-byte aligned");
     CHECK_ARG(count <= 1 || stride_bytes >= gcc_msg_bytes(h->cap, cap_others), "stride smaller than a message");
     CHECK_ARG(count <= kMaxPeers, "at most 64 messages per call");
+    if (h->tune.fail_absorb > 0 && --h->tune.fail_absorb == 0)
+        return set_err(GCC_E_INTERNAL, "gcc_forest_absorb_many: injected failure (tune key fail_absorb)");
     DeviceGuard g(h->device);
     int rc = flush(h);
     if (rc) return rc;
@@ -3735,6 +3740,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     }
     else if (k == "fold_release") t.fold_release = (int)value;
     else if (k == "post_check") t.post_check = std::max(0, std::min(2, (int)value));
+    else if (k == "fail_absorb") t.fail_absorb = std::max(0, (int)value);
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;

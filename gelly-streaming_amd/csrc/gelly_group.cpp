@@ -50,7 +50,18 @@ Rccl& rccl() {
     static Rccl r;
     static std::once_flag once;
     std::call_once(once, [] {
-        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        // GELLY_RCCL_LIB: another library with RCCL's ABI in its place — the tests' shared-memory stand-in
+        // (tests/cpp/shm_rccl.cpp), which runs this file's merge loop with several ranks on one GPU or on CPU
+        const char* alt = getenv("GELLY_RCCL_LIB");
+        void* h = nullptr;
+        if (alt && *alt) {
+            h = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
+            if (!h) {
+                r.error = std::string("dlopen ") + alt + " (GELLY_RCCL_LIB): " + dlerror();
+                return;
+            }
+        }
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
         if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
         if (!h) {
             r.error = std::string("dlopen librccl.so.1: ") + dlerror();
@@ -114,23 +125,31 @@ struct gcc_comm {
     u64 cap_others = 0;    // the speculative list capacity (grows on overflow, shrinks slowly)
     bool prefer_labels = false;
     u64 last_bytes = 0;    // bytes each rank contributed to the last merge's all_gather
-    int last_rounds = 0;
+    int last_rounds = 0;   // all_gathers of the last merge (compact rounds + the label exchange)
+    bool last_labels = false;  // the last merge ended with the label exchange
     // a merge failed where the ranks could not agree on it (e.g. a buffer allocation before the collective): the
     // communicator was aborted and is unusable; the peers may be left inside the collective, so the job's ranks must
     // all be torn down (as a failed Flink task restarts the job)
     bool broken = false;
+    // this rank's forest failed to absorb the peers AFTER the last collective of a merge (the absorb / compress of the
+    // final round): the peers' merges succeeded, this rank's returned the error. Sticky: every later merge on this
+    // communicator starts from that failure, so the peers learn of it in-band in their next merge (a failed-status
+    // header or agree()) and every rank returns an error there — no rank is left waiting in a collective for a rank
+    // that stopped calling
+    bool poisoned = false;
 };
 
 namespace {
 
-// Grow a buffer. The new one is allocated before the old one is freed, so a failed allocation leaves the buffer as it
-// was: every rank's buffers stay at least as large as the sizes the ranks last agreed on (gcc_comm::agreed_msg).
+// Grow a buffer: the old one is freed first, so the peak is the new size (the label exchange's receive buffer is
+// nranks x V x 4 B: 2 GiB at 8 ranks and 2^26 ids). A failed allocation leaves the buffer empty; the caller then
+// resets gcc_comm::agreed_msg, so the next merge allocates and agrees again.
 int ensure(void*& p, u64& have, u64 need) {
     if (have >= need) return GCC_OK;
-    void* q = nullptr;
-    HIP_TRY(hipMalloc(&q, (size_t)need));
     if (p) (void)hipFree(p);
-    p = q;
+    p = nullptr;
+    have = 0;
+    HIP_TRY(hipMalloc(&p, (size_t)need));
     have = need;
     return GCC_OK;
 }
@@ -187,6 +206,12 @@ int agree(gcc_comm* c, hipStream_t st, int local_rc, int* failed) {
     return GCC_OK;
 }
 
+// An error of this rank's own after the merge's last collective (gcc_comm::poisoned)
+int own_error(gcc_comm* c, int rc) {
+    c->poisoned = true;
+    return rc;
+}
+
 // local_rc (this rank's own error, or 0) and the peers' statuses -> the error every rank returns, or 0
 int agreed_error(int local_rc, int failed) {
     if (local_rc) return local_rc;
@@ -200,19 +225,22 @@ int merge_labels_rccl(gcc_forest* h, gcc_comm* c, u32 V, hipStream_t st, int loc
     const u32* lab = nullptr;
     int rc = local_rc;
     if (!rc) rc = gcc_forest_labels_device(h, &lab);
-    if (!rc) rc = ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * V * sizeof(u32));
+    if (!rc) {
+        rc = ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * V * sizeof(u32));
+        if (rc) c->agreed_msg = 0;  // the receive buffer is gone: a later compact round allocates and agrees again
+    }
     int failed = -1;
     ABI_TRY(agree(c, st, rc, &failed));
     if (rc || failed >= 0) return agreed_error(rc, failed);
     const ncclResult_t r = rccl().AllGather(lab, c->d_recv, V, ncclUint32, c->comm, st);
     if (r != ncclSuccess)
         return fail_comm(c, gcc_set_err(GCC_E_HIP, "ncclAllGather (labels): %s", rccl().GetErrorString(r)));
-    for (int p = 0; p < c->nranks; ++p)
-        if (p != c->rank)
-            ABI_TRY(gcc_forest_merge_labels_device(h, static_cast<const u32*>(c->d_recv) + (u64)p * V, V));
-    ABI_TRY(gcc_forest_compress(h));
     c->last_bytes = 4ull * V;
-    return GCC_OK;
+    int rc2 = GCC_OK;
+    for (int p = 0; p < c->nranks && !rc2; ++p)
+        if (p != c->rank) rc2 = gcc_forest_merge_labels_device(h, static_cast<const u32*>(c->d_recv) + (u64)p * V, V);
+    if (!rc2) rc2 = gcc_forest_compress(h);
+    return rc2 ? own_error(c, rc2) : GCC_OK;
 }
 
 }  // namespace
@@ -294,6 +322,14 @@ int gcc_comm_info(gcc_comm* c, int* nranks, int* rank, uint64_t* last_bytes) {
     return GCC_OK;
 }
 
+int gcc_comm_last_merge(gcc_comm* c, int* rounds, int* labels, uint64_t* cap_others) {
+    CHECK_ARG(c, "null comm");
+    if (rounds) *rounds = c->last_rounds;
+    if (labels) *labels = c->last_labels ? 1 : 0;
+    if (cap_others) *cap_others = c->cap_others;
+    return GCC_OK;
+}
+
 // Collective: every rank calls it with its forest (same id_capacity everywhere); afterwards every rank's forest is
 // the union of all of them, compressed. Synchronises the forest's stream (it reads the gathered headers).
 int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
@@ -309,11 +345,14 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
     if (!c->h_hdr) HIP_TRY(hipHostMalloc((void**)&c->h_hdr, (size_t)c->nranks * 16, hipHostMallocDefault));
     if (c->cap_others == 0) c->cap_others = std::max<u64>(1024, V / 64);
     c->last_rounds = 0;
+    c->last_labels = false;
     // Every rank takes the same decisions (sizes, repeats) from the gathered headers. A rank whose own encode, absorb
     // or compress fails keeps following them: in a next compact round it sends a failed-status header
     // (include/gelly_cc.h), before a round that grows the buffers and before the label exchange the ranks agree
     // (agree()), so every rank leaves together with an error instead of one rank leaving its peers in a collective.
-    int local_rc = GCC_OK;
+    int local_rc = c->poisoned ? gcc_set_err(GCC_E_INTERNAL, "an earlier group merge failed on this rank (its forest is "
+                                                              "not the union of the ranks'): destroy the group")
+                               : GCC_OK;
     while (!c->prefer_labels) {
         const u64 cap = c->cap_others;
         const u64 size = round16(gcc_msg_bytes(V, cap));
@@ -326,6 +365,7 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
         if (size > c->agreed_msg) {
             int rc = ensure(c->d_send, c->send_bytes, size);
             if (!rc) rc = ensure(c->d_recv, c->recv_bytes, (u64)c->nranks * size);
+            if (rc) c->agreed_msg = 0;  // a buffer may be gone: the next merge allocates and agrees again
             int failed = -1;
             ABI_TRY(agree(c, st, rc ? rc : local_rc, &failed));
             if (rc || failed >= 0) return agreed_error(rc ? rc : local_rc, failed);
@@ -361,11 +401,12 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
             return local_rc ? local_rc : gcc_set_err(GCC_E_INTERNAL, "group merge: rank %d failed (its error is on that rank)", failed);
         if (nmax <= cap) {
             if (4 * nmax < cap && cap > 1024) c->cap_others = std::max<u64>({1024, 3 * nmax / 2, cap / 2});
-            return local_rc;  // the peers finish too: an error here is this rank's own
+            return local_rc ? own_error(c, local_rc) : GCC_OK;  // the peers finish: an error here is this rank's own
         }
         c->cap_others = std::max<u64>(3 * nmax / 2, 2 * cap);  // some list did not fit: again, larger
     }
     ++c->last_rounds;
+    c->last_labels = true;
     return merge_labels_rccl(h, c, V, st, local_rc);
 }
 

@@ -5,40 +5,26 @@ partial DisjointSet, Kryo-serialised, to ONE task: ``timeWindowAll(t).reduce(Com
 parallelism-1 ``Merger`` (…/SummaryAggregation.java:107-119). SummaryTreeReduce (…/SummaryTreeReduce.java:95-123)
 pairs partitions up in a log2 tree instead.
 
-MI355X form: every rank (one process per GPU) keeps a full-range forest. At a window boundary each rank
-compresses its forest to canonical min-id labels and encodes it as a compact message (include/gelly_cc.h:
-header, bitmap of the largest component, (v, label) list of the other seen ids — 1/32 of the label array
-when one component dominates). One RCCL all_gather over xGMI moves every rank's message to every rank
-(the list capacity is speculative — the last window's need x1.5 — and the gathered headers say whether a
-repair round is needed), and each rank absorbs the P-1 partitions into its own forest. Every rank ends with the global partition — exactly the forest the reference's reduce +
-Merger emit — in one collective, with no serial bottleneck. When the compact form is not smaller than the
-label array (no dominant component), the labels themselves are exchanged: a butterfly of log2(P) rounds of
-RCCL send/recv with rank ^ 2^r for a power-of-two world, all_gather otherwise.
+MI355X form: every rank (one process per GPU) keeps a full-range forest, and the whole merge runs inside
+libgelly_cc (csrc/gelly_group.cpp, ``gcc_forest_group_merge``) over its own RCCL communicator: each rank compresses
+and encodes its forest as a compact message (include/gelly_cc.h: header, bitmap of the largest component, (v, label)
+list of the other seen ids), ONE ncclAllGather over xGMI moves every message to every rank, and each rank absorbs
+the P-1 others on its device. The list capacity is speculative (the last window's need x1.5; the gathered headers
+say whether a repeat round is needed); when the compact form stops paying, the label arrays are all-gathered. Every
+rank ends with the global partition — the forest the reference's reduce + Merger emit — with no serial bottleneck.
+torch.distributed only carries the communicator's unique id (bootstrap bytes); it is never on the data path, and
+this module has no second (Python) implementation of the protocol: with several ranks on ONE device (tests, the
+one-GPU rehearsal) GELLY_RCCL_LIB points the same C++ loop at the shared-memory stand-in tests/cpp/shm_rccl.cpp.
 """
 from __future__ import annotations
 
 import ctypes
-import os
-from typing import Optional, Protocol, Sequence
-
-
-class ExchangeForest(Protocol):
-    """What the merge needs from a forest."""
-
-    id_capacity: int
-
-    def compress(self) -> None: ...                     # canonicalise (async on the comm stream)
-    def exchange_tensor(self): ...                      # torch tensor holding the labels (same device as comms)
-    def absorb(self, labels) -> None: ...               # forest := forest ∪ {(v, labels[v])}
-    def new_bytes(self, n: int): ...                    # uint8 tensor of n bytes on the comm device
-    def encode(self, msg, cap_others: int) -> None: ... # compress + write the message into msg
-    def absorb_msg(self, msg, cap_others: int) -> None: ...  # forest := forest ∪ the message's partition
-    def absorb_msgs(self, msgs, stride: int, count: int, skip: int, cap_others: int) -> None: ...  # all but `skip`
+from typing import Optional, Sequence
 
 
 class TorchDisjointSet:
     """A DisjointSet whose two id-range buffers are torch tensors on this rank's GPU and whose HIP stream is
-    torch's current stream, so RCCL collectives issued by torch.distributed order correctly with the kernels."""
+    torch's current stream, so that torch work (events, the bench's barriers) orders with the forest's kernels."""
 
     def __init__(self, id_capacity: int, device: int = 0):
         import torch
@@ -51,33 +37,7 @@ class TorchDisjointSet:
         self.ds = DisjointSet(self.id_capacity, self.device, d_buffers=(self.bufs[0].data_ptr(), self.bufs[1].data_ptr()))
         self.ds.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
-    # ExchangeForest
-    def compress(self) -> None:
-        self.ds.compress()
-
-    def exchange_tensor(self):
-        """The tensor holding the canonical labels (read-only view: the forest's incremental-compress state stays)."""
-        cur = self.ds.labels_device()
-        return self.bufs[0] if self.bufs[0].data_ptr() == cur else self.bufs[1]
-
-    def absorb(self, labels) -> None:
-        self.ds.merge_labels_device(labels.data_ptr(), labels.numel())
-
-    def new_bytes(self, n: int):
-        import torch
-
-        return torch.empty(int(n), dtype=torch.uint8, device=f"cuda:{self.device}")
-
-    def encode(self, msg, cap_others: int) -> None:
-        self.ds.encode_message(msg.data_ptr(), cap_others)
-
-    def absorb_msg(self, msg, cap_others: int) -> None:
-        self.ds.absorb_message(msg.data_ptr(), cap_others)
-
-    def absorb_msgs(self, msgs, stride: int, count: int, skip: int, cap_others: int) -> None:
-        self.ds.absorb_messages(msgs.data_ptr(), stride, count, skip, cap_others)
-
-    def __getattr__(self, name):  # delegate the DisjointSet surface (find, getMatches, fold_device, ...)
+    def __getattr__(self, name):  # delegate the DisjointSet surface (find, getMatches, fold_device, compress, ...)
         return getattr(self.ds, name)
 
 
@@ -134,6 +94,16 @@ class RcclComm:
         call("gcc_comm_info", self._h, None, None, ctypes.byref(b))
         return b.value
 
+    def last_merge(self) -> dict:
+        """The last merge: all_gathers it took (compact rounds + the label exchange), whether it ended with the
+        label exchange, the bytes each rank contributed to its last all_gather, the next merge's list capacity."""
+        from .native import call
+
+        rounds, labels, cap = ctypes.c_int(), ctypes.c_int(), ctypes.c_uint64()
+        call("gcc_comm_last_merge", self._h, ctypes.byref(rounds), ctypes.byref(labels), ctypes.byref(cap))
+        return {"rounds": rounds.value, "labels": bool(labels.value), "bytes": self.last_bytes(),
+                "cap_others": cap.value}
+
     def close(self) -> None:
         from .native import call
 
@@ -161,179 +131,35 @@ def group_merge(forests: Sequence, comms: Optional[Sequence[RcclComm]] = None) -
         f._dirty()
 
 
-def _round16(n: int) -> int:
-    return (int(n) + 15) // 16 * 16
-
-
 class ForestGroup:
-    """Cross-rank merge of one forest per rank (mode "auto": compact all_gather, label exchange fallback;
-    "labels": always exchange label arrays)."""
+    """Cross-rank merge of one forest per rank: SummaryBulkAggregation's timeWindowAll(t).reduce(CombineCC) + Merger
+    (…/SummaryBulkAggregation.java:81-83) over every rank of a torch.distributed group. Rank 0 creates the RCCL unique
+    id, torch.distributed broadcasts its bytes (any backend: nccl, or gloo for rehearsals), and every merge is
+    gcc_forest_group_merge on this rank's communicator."""
 
-    def __init__(self, group=None, mode: str = "auto", transport: str = "auto", device: Optional[int] = None):
-        """transport "rccl": the merge runs in libgelly_cc over its own RCCL communicator (gcc_forest_group_merge);
-        "torch": the same protocol driven from Python over torch.distributed (gloo rehearsals on CPU); "auto": rccl
-        when the group's backend is nccl (= RCCL) unless GELLY_MERGE=torch."""
+    def __init__(self, group=None, device: Optional[int] = None):
+        import torch
         import torch.distributed as dist
 
-        if mode not in ("auto", "labels"):
-            raise ValueError(f"unknown merge mode {mode!r}")
-        self._dist = dist
         self.group = group
-        self.mode = mode
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.comm: Optional[RcclComm] = None
-        if transport == "auto":
-            backend = str(dist.get_backend(group)).lower()
-            transport = "rccl" if backend == "nccl" and os.environ.get("GELLY_MERGE", "") != "torch" else "torch"
-        if transport == "rccl" and mode == "auto":
-            import torch
+        dev = torch.cuda.current_device() if device is None else int(device)
+        uid = [RcclComm.unique_id() if self.rank == 0 else None]
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        dist.broadcast_object_list(uid, src=src, group=group)  # bootstrap bytes only
+        self.comm = RcclComm(dev, self.world, self.rank, uid[0])
+        self.last = {}  # what the last merge did (measurement / tests): RcclComm.last_merge()
 
-            dev = torch.cuda.current_device() if device is None else int(device)
-            uid = [RcclComm.unique_id() if self.rank == 0 else None]
-            dist.broadcast_object_list(uid, src=self._global(0), group=group)  # bootstrap bytes only
-            self.comm = RcclComm(dev, self.world, self.rank, uid[0])
-        self.transport = transport
-        self._recv = None
-        self._gather = None
-        self._cap = 0          # list capacity of the message buffer (grows, never shrinks)
-        self._msg = None
-        self._recv_msg = None
-        self._hdr_host = None
-        self._hdr_event = None
-        self._prefer_labels = False  # the compact form did not pay: exchange labels from now on
-        self.last = {}         # what the last merge sent (measurement / tests)
-
-    def _global(self, r: int) -> int:
-        return r if self.group is None else self._dist.get_global_rank(self.group, r)
-
-    def _recv_like(self, t):
-        if self._recv is None or self._recv.shape != t.shape or self._recv.device != t.device:
-            self._recv = t.new_empty(t.shape)
-        return self._recv
-
-    def _all_gather_flat(self, out, inp) -> None:
-        """out (world * inp.numel()) := concatenation of every rank's inp (RCCL: one allgather)."""
-        try:
-            self._dist.all_gather_into_tensor(out, inp, group=self.group)
-        except (RuntimeError, AttributeError, NotImplementedError):  # backends without the flat form (gloo)
-            n = inp.numel()
-            self._dist.all_gather([out[r * n:(r + 1) * n] for r in range(self.world)], inp, group=self.group)
-
-    def merge_forest(self, forest: ExchangeForest) -> None:
+    def merge_forest(self, forest) -> None:
         """forest := union of every rank's forest (collective: every rank must call it)."""
-        if self.comm is not None:  # the whole merge inside libgelly_cc, over RCCL
-            self.comm.merge(forest.ds if hasattr(forest, "ds") else forest)
-            self.last = {"compact": True, "bytes": self.comm.last_bytes(), "transport": "rccl"}
-            return
-        forest.compress()
-        if self.world == 1:
-            return
-        if self.mode == "auto" and self._merge_compact(forest):
-            return
-        self._merge_labels(forest)
-        self.last = {"compact": False, "rounds": 1, "full_bytes": 4 * int(forest.id_capacity)}
-
-    def _merge_compact(self, forest: ExchangeForest) -> bool:
-        """One all_gather of messages at a speculative list capacity; absorb + compress are enqueued before the
-        host looks at the gathered headers. If some rank's list did not fit, the (exact, since union is
-        idempotent) exchange is repeated with a larger capacity; if the compact form stops paying, the label
-        exchange finishes the merge and later merges go straight to it."""
-        from .native import MSG_HEADER_BYTES, msg_bytes
-
-        if self._prefer_labels:
-            return False
-        V = int(forest.id_capacity)
-        full = 4 * V
-        if self._cap == 0:
-            self._cap = max(1024, V // 64)
-        rounds = 0
-        while True:
-            cap = self._cap
-            size = _round16(msg_bytes(V, cap))
-            if size >= full:
-                self._prefer_labels = True
-                if rounds == 0:
-                    return False
-                self._merge_labels(forest)  # finish exactly (the forest already holds a partial union)
-                self.last.update(compact=False, rounds=rounds + 1)
-                return True
-            if self._msg is None or self._msg.numel() < size:
-                self._msg = forest.new_bytes(size)
-            if self._recv_msg is None or self._recv_msg.numel() < self.world * size:
-                self._recv_msg = forest.new_bytes(self.world * size)
-            forest.encode(self._msg, cap)
-            recv = self._recv_msg[:self.world * size]
-            self._all_gather_flat(recv, self._msg[:size])
-            hdrs = self._copy_headers(recv.view(self.world, size)[:, :MSG_HEADER_BYTES])
-            forest.absorb_msgs(recv, size, self.world, self.rank, cap)
-            forest.compress()
-            counts = self._wait_headers(hdrs)[:, 1]
-            nmax = int(counts.max())
-            rounds += 1
-            self.last = {"n_others": [int(c) for c in counts], "cap": cap, "bytes": size, "full_bytes": full,
-                         "compact": True, "rounds": rounds}
-            if nmax <= cap:
-                if 4 * nmax < cap and cap > 1024:  # shrink slowly toward 1.5x the observed need
-                    self._cap = max(1024, 3 * nmax // 2, cap // 2)
-                return True
-            self._cap = max(3 * nmax // 2, 2 * cap)
-
-    def _copy_headers(self, hdr_view):
-        """Start the device->host copy of the gathered headers (pinned, async) and return a handle."""
-        import torch
-
-        h = hdr_view.contiguous()
-        if h.device.type == "cpu":
-            return h.clone()
-        if self._hdr_host is None or self._hdr_host.shape != h.shape:
-            self._hdr_host = torch.empty(h.shape, dtype=h.dtype, pin_memory=True)
-        self._hdr_host.copy_(h, non_blocking=True)
-        self._hdr_event = torch.cuda.Event()
-        self._hdr_event.record()
-        return self._hdr_host
-
-    def _wait_headers(self, h):
-        if self._hdr_event is not None:
-            self._hdr_event.synchronize()
-            self._hdr_event = None
-        return h.numpy().view("<u4").reshape(self.world, 4)
-
-    def _merge_labels(self, forest: ExchangeForest) -> None:
-        dist = self._dist
-        buf = forest.exchange_tensor()
-        if self.world & (self.world - 1) == 0:
-            recv = self._recv_like(buf)
-            step = 1
-            while step < self.world:
-                buf = forest.exchange_tensor()  # compress swaps buffers: fetch the current labels every round
-                partner = self._global(self.rank ^ step)
-                ops = [dist.P2POp(dist.isend, buf, partner, self.group), dist.P2POp(dist.irecv, recv, partner, self.group)]
-                if self._gloo_cuda(buf):  # gloo's P2P on CUDA tensors is not ordered with the stream: fence both sides
-                    import torch
-
-                    torch.cuda.synchronize(buf.device)
-                for req in dist.batch_isend_irecv(ops):
-                    req.wait()
-                if self._gloo_cuda(buf):
-                    torch.cuda.synchronize(buf.device)
-                forest.absorb(recv)
-                forest.compress()
-                step <<= 1
-        else:
-            if self._gather is None or self._gather[0].shape != buf.shape:
-                self._gather = [buf.new_empty(buf.shape) for _ in range(self.world)]
-            dist.all_gather(self._gather, buf, group=self.group)
-            for p, t in enumerate(self._gather):
-                if p != self.rank:
-                    forest.absorb(t)
-            forest.compress()
-
-    def _gloo_cuda(self, t) -> bool:
-        """A CUDA tensor over the gloo backend (one-GPU rehearsals of the N > 1 path)."""
-        return t.device.type == "cuda" and self._dist.get_backend(self.group) == "gloo"
+        self.comm.merge(forest.ds if hasattr(forest, "ds") else forest)
+        self.last = self.comm.last_merge()
 
     def reduce(self, summary, combineFun=None):
         """SummaryBulkAggregation's timeWindowAll(...).reduce(combineFun) across ranks, for a forest summary."""
         self.merge_forest(summary)
         return summary
+
+    def close(self) -> None:
+        self.comm.close()

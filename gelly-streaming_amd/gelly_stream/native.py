@@ -11,7 +11,8 @@ import os
 from ctypes import POINTER, byref, c_char_p, c_float, c_int, c_uint32, c_uint64, c_void_p
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# GELLY_CC_LIB: an alternative build of the same ABI (A/B measurements of kernel variants only)
+# GELLY_CC_LIB: an alternative build of the same ABI (A/B measurements of kernel variants; the CPU tests' host build
+# of the group merge, tests/cpp/build/libgelly_group_host.so, which exports only the merge's part of the ABI)
 LIB_PATH = os.environ.get("GELLY_CC_LIB") or os.path.join(PKG_ROOT, "lib", "libgelly_cc.so")
 
 UNSEEN = 0xFFFFFFFF
@@ -70,6 +71,7 @@ _SIGS = {
     "gcc_comm_init_all": (c_int, [c_int, c_void_p, c_void_p]),
     "gcc_comm_destroy": (c_int, [c_void_p]),
     "gcc_comm_info": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_uint64)]),
+    "gcc_comm_last_merge": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_uint64)]),
     "gcc_forest_group_merge": (c_int, [c_void_p, c_void_p]),
     "gcc_group_merge": (c_int, [c_void_p, c_int, c_void_p]),
     "gcc_forest_device_ptr": (c_int, [c_void_p, POINTER(c_void_p)]),
@@ -168,7 +170,10 @@ def lib() -> ctypes.CDLL:
         if not os.path.exists(LIB_PATH):
             raise GellyCCError(-3, "load", f"{LIB_PATH} not found: build it first (__graft_entry__.build())")
         l = ctypes.CDLL(LIB_PATH)
+        partial = bool(os.environ.get("GELLY_CC_LIB"))
         for name, (res, args) in _SIGS.items():
+            if partial and not hasattr(l, name):
+                continue  # an alternative build may carry part of the ABI; calling a missing symbol raises
             fn = getattr(l, name)
             fn.restype = res
             fn.argtypes = args

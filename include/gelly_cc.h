@@ -154,7 +154,8 @@ int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_by
  * Merger (…/SummaryBulkAggregation.java:81-83, …/SummaryAggregation.java:107-119). One communicator per GPU over
  * RCCL (xGMI); every rank's forest becomes the union of all ranks' forests — ONE all_gather of the compact messages
  * above (label arrays when no component dominates), each rank absorbing the others itself. RCCL is loaded at run
- * time (dlopen librccl.so.1; a process that already mapped one, e.g. torch's, shares it). */
+ * time (dlopen librccl.so.1; a process that already mapped one, e.g. torch's, shares it; the environment variable
+ * GELLY_RCCL_LIB names another library with RCCL's ABI instead — the tests' shared-memory stand-in). */
 typedef struct gcc_comm gcc_comm;
 #define GCC_COMM_ID_BYTES 128 /* = the RCCL unique id */
 /* rank 0 creates the id and hands its bytes to every rank over any channel (torch.distributed, the JVM, a file) */
@@ -164,6 +165,9 @@ int gcc_comm_init_all(int ndev, const int* devices, gcc_comm** comms_out);      
 int gcc_comm_destroy(gcc_comm* c);
 /* nranks, rank, and the bytes each rank contributed to the last merge's all_gather (any may be NULL) */
 int gcc_comm_info(gcc_comm* c, int* nranks, int* rank, uint64_t* last_bytes);
+/* the last gcc_forest_group_merge: its all_gathers (compact rounds, + 1 for the label exchange), whether it ended with
+ * the label exchange, and the speculative list capacity the next merge starts from (any may be NULL) */
+int gcc_comm_last_merge(gcc_comm* c, int* rounds, int* labels, uint64_t* cap_others);
 /* collective over the communicator's ranks (every rank calls it with its forest, same id_capacity); synchronises
  * the forest's stream. Afterwards every rank's forest holds the global partition, compressed. */
 int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c);
@@ -299,7 +303,8 @@ int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, 
  * inc_min_ids, inc_div, inc_inplace, inc_check, post_check, inc_split, fold_release, experimental, refresh_labels, bucket,
  * bucket_min_batch, bucket_min_ids, bucket_levels, bucket_sample, bucket_hub_sample, bucket_p1, bucket_p2_per, bucket_p2_vw,
  * bucket_chunk, bucket_windows, bucket_items,
- * bucket_slow2, bucket_defer, pin_chunk, lds_edges_per_word. Unknown keys return GCC_E_INVALID.
+ * bucket_slow2, bucket_defer, pin_chunk, lds_edges_per_word; fail_absorb (tests: the n-th next absorb fails with
+ * GCC_E_INTERNAL before launching anything). Unknown keys return GCC_E_INVALID.
  * One setting is known to give wrong results and is refused (GCC_E_INVALID) unless `experimental` is set to 1 first:
  * inc_split = 1 (path splitting in the recording fold before an in-place incremental compress: round 3's stale label,
  * kept only to reproduce it). */
