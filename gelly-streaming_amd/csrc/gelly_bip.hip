@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void signed_fold_giant_kernel(u32* __restrict_
 // fails the result (Candidates.merge :78-81).
 __global__ __launch_bounds__(256) void signed_merge_kernel(u32* __restrict__ word, const u32* __restrict__ other, u32 n,
                                                           u32* __restrict__ fail, const u32* __restrict__ other_fail) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && *other_fail) *fail = 1u;
+    if (other_fail && blockIdx.x == 0 && threadIdx.x == 0 && *other_fail) *fail = 1u;
     const u64 stride = (u64)gridDim.x * 256;
     for (u64 v = (u64)blockIdx.x * 256 + threadIdx.x; v < n; v += stride) {
         const u32 w = other[v];
@@ -475,7 +475,7 @@ int gcc_signed_merge_words(gcc_signed* into, const uint32_t* d_words, uint32_t n
     if (n) {
         // the other forest's (v, parent, parity) triples as constraints; its fail word is the flag above
         hipLaunchKernelGGL(signed_merge_kernel, dim3(grid_for_n(n, kMaxGrid)), dim3(256), 0, into->stream, into->d_word,
-                           d_words, n, into->d_fail, into->d_fail);
+                           d_words, n, into->d_fail, nullptr);  // other_failed: the memset above
         HIP_TRY(hipGetLastError());
     }
     into->compressed = false;

@@ -560,12 +560,19 @@ static inline unsigned chunk_grid(u64 n, int per_wave, int block, unsigned max_b
     return (unsigned)(b < 1 ? 1 : (b > max_blocks ? max_blocks : b));
 }
 
+// SPLIT: the finds split paths in `parent` (plain stores). Only the mid-fold refresh (labels == nullptr) does: it
+// shortens the chains the rest of the fold walks. A compress that writes labels uses read-only finds (round 5): its
+// split stores went into the buffer that becomes the spare after the swap, i.e. the OUTPUT of the compress two kernels
+// later, and a plain store landing that late would overwrite a label (the host replay's late-store model,
+// tests/cpp/test_uf_replay.cpp). tune key compress_split = 1 restores them (A/B only).
+template <bool SPLIT>
 __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__ parent, u32* __restrict__ labels, u32 n,
                                                                const u32* __restrict__ giant_prev,
                                                                u32* __restrict__ giant_next, u64* __restrict__ bits,
                                                                u32* __restrict__ bloom_clear, u64* __restrict__ oth,
                                                                const u64* __restrict__ newbits) {
     trace_start(kTrCompressBits);
+    typedef gcc::UnionFind<gcc::LoadPlain, SPLIT> CF;
     __shared__ u32 s_g, s_g0;
     NoCount c;
     const u32 lane = threadIdx.x & 63;
@@ -587,7 +594,7 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
             atomicAnd(&bloom_clear[w], 0u);
     if (threadIdx.x == 0) {
         const u32 g0 = giant_prev ? *giant_prev : UNSEEN;
-        s_g = (g0 == UNSEEN) ? UNSEEN : UF::find_from(parent, g0, parent[g0], c);
+        s_g = (g0 == UNSEEN) ? UNSEEN : CF::find_from(parent, g0, parent[g0], c);
         s_g0 = g0;
         if (blockIdx.x == 0 && giant_next) *giant_next = s_g;
     }
@@ -610,10 +617,10 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
             const u32x4 p = cur[k];
             u32 lab[4];
             // a child of the tracked root g (a root during the compress) needs no find: most ids of a giant
-            lab[0] = (p.x >= v0 || p.x == g) ? p.x : (p.x == g0 ? g : UF::find_from(parent, v0, p.x, c));
-            lab[1] = (p.y >= v0 + 1 || p.y == g) ? p.y : (p.y == g0 ? g : UF::find_from(parent, v0 + 1, p.y, c));
-            lab[2] = (p.z >= v0 + 2 || p.z == g) ? p.z : (p.z == g0 ? g : UF::find_from(parent, v0 + 2, p.z, c));
-            lab[3] = (p.w >= v0 + 3 || p.w == g) ? p.w : (p.w == g0 ? g : UF::find_from(parent, v0 + 3, p.w, c));
+            lab[0] = (p.x >= v0 || p.x == g) ? p.x : (p.x == g0 ? g : CF::find_from(parent, v0, p.x, c));
+            lab[1] = (p.y >= v0 + 1 || p.y == g) ? p.y : (p.y == g0 ? g : CF::find_from(parent, v0 + 1, p.y, c));
+            lab[2] = (p.z >= v0 + 2 || p.z == g) ? p.z : (p.z == g0 ? g : CF::find_from(parent, v0 + 2, p.z, c));
+            lab[3] = (p.w >= v0 + 3 || p.w == g) ? p.w : (p.w == g0 ? g : CF::find_from(parent, v0 + 3, p.w, c));
             if (newbits) {  // an absorb's deferred new ids (msg_absorb_bits_kernel): still UNSEEN, in g's component
                 const u32 nb = (u32)(newbits[v0 >> 6] >> (v0 & 63)) & 15u;
                 if (nb) {
@@ -635,7 +642,8 @@ __global__ __launch_bounds__(kBlock) void compress_bits_kernel(u32* __restrict__
         u32 lab[4] = {UNSEEN, UNSEEN, UNSEEN, UNSEEN};
         for (u32 k = 0; k < 4; ++k)
             if (v0 + k < n) {
-                lab[k] = gcc::compress_label(parent, (u32)(v0 + k));
+                const u32 pk = parent[v0 + k];
+                lab[k] = pk >= (u32)(v0 + k) ? pk : CF::find_from(parent, (u32)(v0 + k), pk, c);
                 if (newbits && lab[k] == UNSEEN && ((newbits[(v0 + k) >> 6] >> ((v0 + k) & 63)) & 1ull)) lab[k] = g;
                 if (labels) labels[v0 + k] = lab[k];
             }
@@ -745,8 +753,14 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
+    // in place, a label is stored write-through (gcc::st_through): the next in-place compress may rewrite the same
+    // slot two kernels later, and a plain store still on its way could land over that
     auto settle = [&](u32 v, u32 p, u32 r) {  // a resolved find: the label and the tracked component's bit
-        if (!INPLACE || r != p) labels[v] = r;
+        if constexpr (INPLACE) {
+            if (r != p) gcc::st_through(labels + v, r);
+        } else {
+            labels[v] = r;
+        }
         if (r == g) __hip_atomic_fetch_or(bits + (v >> 6), 1ull << (v & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto flush = [&]() {
@@ -835,7 +849,8 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
             if (v0 + k < n) {
                 const u32 pk = parent[v0 + k];
                 lab[k] = inc_label(parent, s_bloom, (u32)(v0 + k), pk);
-                if (!INPLACE || lab[k] != pk) labels[v0 + k] = lab[k];
+                if (!INPLACE) labels[v0 + k] = lab[k];
+                else if (lab[k] != pk) gcc::st_through(labels + v0 + k, lab[k]);
             }
         chunk_bits(bits, nwords, nfull, lane, g, lab);
     }
@@ -1805,6 +1820,9 @@ struct FoldTune {
     // tests only: the fail_absorb-th next gcc_forest_absorb_many call fails with GCC_E_INTERNAL before it launches
     // anything (0: never) — a rank's absorb failing inside the cross-GPU group merge (tests/test_gpu_group.py)
     int fail_absorb = 0;
+    // the full compress's finds: read-only (0, round 5) or splitting paths in the old buffer (1, rounds 1-4; A/B only —
+    // compress_bits_kernel says why not)
+    int compress_split = 0;
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -2122,9 +2140,13 @@ static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth =
     bool inplace = false;  // the compress rewrote d_parent itself (no swap)
     const bool inc_here = inc_forest(h) && !oth && !newbits;  // masks in or out: a full compress
     if (!h->filter_enabled()) {
-        rc = launch_k(h, name, 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)), dim3(kBlock), 0,
-                      h->d_parent, h->d_spare, h->cap, (const u32*)nullptr, (u32*)nullptr, (u64*)nullptr, (u32*)nullptr,
-                      (u64*)nullptr, (const u64*)nullptr);
+        rc = h->tune.compress_split
+                 ? launch_k(h, name, 0, compress_bits_kernel<true>, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)),
+                            dim3(kBlock), 0, h->d_parent, h->d_spare, h->cap, (const u32*)nullptr, (u32*)nullptr,
+                            (u64*)nullptr, (u32*)nullptr, (u64*)nullptr, (const u64*)nullptr)
+                 : launch_k(h, name, 0, compress_bits_kernel<false>, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)),
+                            dim3(kBlock), 0, h->d_parent, h->d_spare, h->cap, (const u32*)nullptr, (u32*)nullptr,
+                            (u64*)nullptr, (u32*)nullptr, (u64*)nullptr, (const u64*)nullptr);
     } else {
         rc = alloc_filter(h);
         if (rc) return rc;
@@ -2168,9 +2190,13 @@ static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth =
             if (!rc && check) rc = inc_check_end(h, inplace ? h->d_spare : h->d_parent, out, bl);
             if (!rc && h->tune.post_check) rc = post_check_launch(h, out, bl);
         } else if (!rc) {
-            rc = launch_k(h, name, 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)), dim3(kBlock), 0,
-                          h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
-                          h->d_giant + (h->giant_slot ^ 1), h->d_bits, clear, oth, newbits);
+            rc = h->tune.compress_split
+                     ? launch_k(h, name, 0, compress_bits_kernel<true>, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)),
+                                dim3(kBlock), 0, h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
+                                h->d_giant + (h->giant_slot ^ 1), h->d_bits, clear, oth, newbits)
+                     : launch_k(h, name, 0, compress_bits_kernel<false>, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)),
+                                dim3(kBlock), 0, h->d_parent, h->d_spare, h->cap, (const u32*)(h->d_giant + h->giant_slot),
+                                h->d_giant + (h->giant_slot ^ 1), h->d_bits, clear, oth, newbits);
             if (oth_done) *oth_done = oth != nullptr;
         }
         h->giant_slot ^= 1;
@@ -2195,7 +2221,7 @@ static int refresh_now(gcc_forest* h) {
         rc = launch_k(h, "vote", 0, giant_vote_kernel, dim3(1), dim3(1024), 0, h->d_parent, h->cap,
                       h->d_giant + h->giant_slot, h->d_giant + 4);
     if (!rc)
-        rc = launch_k(h, "refresh_bits", 0, compress_bits_kernel, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)),
+        rc = launch_k(h, "refresh_bits", 0, compress_bits_kernel<true>, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)),
                       dim3(kBlock), 0, h->d_parent, (u32*)nullptr, h->cap, (const u32*)(h->d_giant + h->giant_slot),
                       h->d_giant + (h->giant_slot ^ 1), h->d_bits, (u32*)nullptr, (u64*)nullptr, (const u64*)nullptr);
     if (rc) return rc;
@@ -3741,6 +3767,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "fold_release") t.fold_release = (int)value;
     else if (k == "post_check") t.post_check = std::max(0, std::min(2, (int)value));
     else if (k == "fail_absorb") t.fail_absorb = std::max(0, (int)value);
+    else if (k == "compress_split") t.compress_split = value != 0;
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;

@@ -44,12 +44,17 @@ struct ReplayHooks {
     // a PLAIN store (not an atomic): the model may let it land again later, after the next kernel's writes (round 4:
     // a plain store of one kernel can become visible after stores of the next one)
     virtual void stored(u32* p, u32 v) { (void)p, (void)v; }
+    // a memory-side ATOMIC changed the word (CAS success, atomicMin lowering it, atomicOr): the model decides whether
+    // a late plain store issued before it may still land over it
+    virtual void atomic(const u32* p) { (void)p; }
 };
 inline ReplayHooks* replay = nullptr;  // null: plain relaxed atomics (product host code never sets it)
 #define UF_REPLAY_BEFORE(p) \
     if (replay) replay->before(p)
 #define UF_REPLAY_WROTE(p, v) \
     if (replay) replay->wrote(p, v)
+#define UF_REPLAY_ATOMIC(p) \
+    if (replay) replay->atomic(p)
 #endif
 
 UF_HD u32 ld(const u32* p) {
@@ -71,12 +76,29 @@ UF_HD void st(u32* p, u32 v) {
     if (replay) replay->stored(p, v);
 #endif
 }
+// A WRITE-THROUGH store (agent-scope relaxed atomic store: global_store ... sc1 on gfx950, which leaves no dirty line in
+// the XCD's L2 — MI355X_MICROARCH.md, store flavours). The in-place incremental compress writes its labels with it:
+// a plain store there could land over the same slot's label of the next in-place compress two kernels later (the late
+// plain stores of DESIGN.md §3; the replay models it as an atomic write).
+UF_HD void st_through(u32* p, u32 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    UF_REPLAY_BEFORE(p);
+    __atomic_store_n(p, v, __ATOMIC_RELAXED);
+    UF_REPLAY_WROTE(p, v);
+    UF_REPLAY_ATOMIC(p);
+#endif
+}
 UF_HD u32 cas(u32* p, u32 cmp, u32 val) {  // returns the old value (fresh: executed at the memory side)
 #if defined(__HIP_DEVICE_COMPILE__)
     return atomicCAS(p, cmp, val);
 #else
     UF_REPLAY_BEFORE(p);
-    if (__atomic_compare_exchange_n(p, &cmp, val, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) UF_REPLAY_WROTE(p, val);
+    if (__atomic_compare_exchange_n(p, &cmp, val, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+        UF_REPLAY_WROTE(p, val);
+        UF_REPLAY_ATOMIC(p);
+    }
     return cmp;
 #endif
 }
@@ -88,7 +110,10 @@ UF_HD u32 amin(u32* p, u32 v) {  // returns the old value
     u32 old = __atomic_load_n(p, __ATOMIC_RELAXED);
     while (old > v && !__atomic_compare_exchange_n(p, &old, v, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
     }
-    if (old > v) UF_REPLAY_WROTE(p, v);
+    if (old > v) {
+        UF_REPLAY_WROTE(p, v);
+        UF_REPLAY_ATOMIC(p);
+    }
     return old;
 #endif
 }
@@ -98,6 +123,7 @@ UF_HD void aor(u32* p, u32 m) {
 #else
     UF_REPLAY_BEFORE(p);
     __atomic_fetch_or(p, m, __ATOMIC_RELAXED);
+    UF_REPLAY_ATOMIC(p);
 #endif
 }
 
@@ -332,11 +358,13 @@ UF_HD void absorb_join(u32* parent, u32 x, u32 R) {
     UF::unite(parent, x, R, c);
 }
 
-// compress_kernel's per-id step (out of place): labels[v] = root(v), UNSEEN stays UNSEEN.
+// compress_kernel's per-id step (out of place): labels[v] = root(v), UNSEEN stays UNSEEN. Read-only find (round 5:
+// compress_bits_kernel<false>; a split store into the old buffer could land over the labels written into it two
+// kernels later, after the buffers swap back).
 UF_HD u32 compress_label(u32* parent, u32 v) {
     NoCount c;
     const u32 p = ld(&parent[v]);
-    return (p >= v) ? p : UF::find_from(parent, v, p, c);
+    return (p >= v) ? p : UFRead::find_from(parent, v, p, c);
 }
 
 // compress_inc_kernel's per-id step: after a compress, parent[] IS the label array; an unmarked parent p is

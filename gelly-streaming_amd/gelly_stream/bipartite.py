@@ -167,6 +167,23 @@ class Candidates:
         """The emission on the device (canonical words in place; asynchronous): what words() copies out."""
         call("gcc_signed_compress", self.handle)
 
+    def device_words_tensor(self):
+        """The canonical words as a torch int32 tensor on this forest's device, copied from the forest's own device
+        buffer (gcc_signed_device_words after a compress; no trip through the host): the send side of merge_group."""
+        import torch
+
+        self.compress()
+        p = c_void_p()
+        call("gcc_signed_device_words", self.handle, byref(p))
+        self.getSuccess()  # synchronises the forest's stream: the compress has written the words
+
+        class _View:  # __cuda_array_interface__ over the forest's buffer (read-only, valid until its next mutation)
+            __cuda_array_interface__ = {"shape": (self.id_capacity,), "typestr": "<i4", "data": (p.value, True),
+                                        "version": 2, "strides": None}
+
+        with torch.cuda.device(self.device):
+            return torch.as_tensor(_View(), device=f"cuda:{self.device}").clone()
+
     def words(self) -> np.ndarray:
         """Canonical words: (component min id << 1) | (sign differs from the minimum's), UNSEEN if unseen."""
         if self._words is None:
@@ -351,9 +368,11 @@ class BipartitenessCheck(SummaryBulkAggregation[Candidates, Candidates]):
 def merge_group(c: Candidates, group=None) -> Candidates:
     """combineFunction across ranks (BipartitenessCheck.java:128-130 over torch.distributed; gloo or RCCL): every
     rank's ``c`` becomes the union of all ranks' summaries, failed if any rank's was. The words travel as one u32 per
-    id (all_gather; the compressed words are the partition's constraints), the fail flags by all_reduce(MAX); each
-    rank then merges its peers' words on its device (gcc_signed_merge_words). The merge is a union, so the order of
-    the peers does not matter and every rank ends with the same canonical words."""
+    id (all_gather; the compressed words are the partition's constraints), the fail flags by all_reduce(MAX) together
+    with the id ranges (every rank must hold the same id_capacity: checked before any words move, so a mismatch is an
+    error on every rank instead of a mismatched all_gather); each rank then merges its peers' words on its device
+    (gcc_signed_merge_words). Over nccl the words are gathered from device memory (device_words_tensor). The merge is
+    a union, so the order of the peers does not matter and every rank ends with the same canonical words."""
     import torch
     import torch.distributed as dist
 
@@ -362,14 +381,21 @@ def merge_group(c: Candidates, group=None) -> Candidates:
     failed = 0 if c.getSuccess() else 1
     on_gpu = dist.get_backend(group) == "nccl"
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
-    flag = torch.tensor([failed], dtype=torch.int32, device=dev)
+    cap = int(c.id_capacity)
+    flag = torch.tensor([failed, cap, -cap], dtype=torch.int64, device=dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-    if int(flag.item()):
+    if int(flag[1].item()) != cap or -int(flag[2].item()) != cap:
+        raise ValueError(f"merge_group: the ranks' id_capacity differ (this rank {cap}, max {int(flag[1].item())}, "
+                         f"min {-int(flag[2].item())})")
+    if int(flag[0].item()):
         c.merge_words(0, 0, other_failed=True)
         return c
     if world == 1:
         return c
-    mine = torch.from_numpy(c.words().view(np.int32)).to(dev)
+    if on_gpu:
+        mine = c.device_words_tensor().to(dev)
+    else:
+        mine = torch.from_numpy(c.words().view(np.int32)).to(dev)
     parts = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(parts, mine, group=group)
     for r, t in enumerate(parts):
@@ -380,4 +406,3 @@ def merge_group(c: Candidates, group=None) -> Candidates:
         c.merge_words(d.data_ptr(), c.id_capacity)
         c.getSuccess()  # synchronises the forest's stream before d is freed
     return c
-

@@ -19,19 +19,24 @@
 //   free ("free"): real concurrent threads (ASan / TSan builds), stale = the word's kernel-start value; big forests.
 //
 // Pipelines (each is the kernel sequence of one product path, gelly_cc.hip):
-//   out            fold_kernel + compress_kernel (out of place: labels into the spare buffer)     [product]
+//   out            fold_kernel + compress_kernel (out of place: labels into the spare buffer;     [product]
+//                  read-only finds since round 5 — argument "split" restores round 4's splitting compress)
 //   inplace_split  fold + a compress IN PLACE with path splitting (round 1's first compress)      [removed]
 //   inplace_nosplit fold + a compress in place, read-only finds                                  [experiment]
 //   inc            fold_kernel<REC> (bloom, no path splitting: UFRec) + compress_inc_kernel<true> [product]
-//                  in place (inc_inplace)
-//   inc_split      the same with path splitting in the recording fold (round 3's product: the     [removed]
-//                  late split store over the in-place compress's root is the stale label)
+//                  in place (inc_inplace), its labels stored write-through (round 5: gcc::st_through)
+//   inc_split      path splitting in the recording fold and plain label stores in the in-place     [removed]
+//                  compress (round 3's product: the late split store over the compress's root is the stale label)
 //   filter         fold_filtered_kernel's round: atomicMin hook + one-round-late settle + ring   [product]
 //                  entries (unite_entry), then the compress
 //   absorb         a peer's merge message: msg_absorb_bits_kernel (plain store of new ids) then  [product]
 //                  msg_absorb_kernel (lists), then the compress
+//   init           a fresh forest's seeded / bucketed start: parent[] := C ? g : UNSEEN by plain   [product]
+//                  stores (bucket_init_kernel, seed_pack_kernel<true>), then the filtered fold, then the compress
 //
-// Input on stdin: V W then W window sizes, then the edges "u v". Args: pipeline mode threads seeds stale_pm [late_pm].
+// Input on stdin: V W then W window sizes, then the edges "u v". Args: pipeline mode threads seeds stale_pm [late_pm
+// [late_depth [any|plain [split|ro]]]]: late stores up to late_depth kernels late, landing over any later write or
+// only over later plain stores, and the full compress's finds splitting paths or read-only.
 // Output: one line per seed with the failing windows, then "pipeline=<p> runs=<n> bad_runs=<k> bad_windows=<m>"
 // and, on the first failure, the id, its label, the expected label and the parent chain. With mode "labels" the
 // sequential reference labels of the last window are printed (one per line) for the oracle cross-check.
@@ -114,22 +119,38 @@ struct Model : gcc::ReplayHooks {
     bool controlled = false;
     unsigned stale_pm = 0;
     unsigned late_pm = 0;
+    // late plain stores (round 5): a store issued in kernel k lands again during kernel k + d,
+    // d drawn from 1..late_depth (2 covers the out-of-place compress's buffer swap: the buffer a kernel stored into is
+    // written again two kernels later). late_any: a late store may land over ANY later write of the word; otherwise
+    // ("plain" flavour) only over later PLAIN stores — a memory-side atomic of a later kernel is ordered after it (the
+    // pattern the MI355X showed: tools/stress_inc.py, a plain split store over the in-place compress's plain store)
+    unsigned late_depth = 1;
+    bool late_any = true;
     Sched sched;
-    // late plain stores: issued in the current kernel (`late`), landing in the next one (`landing`, at op `at`)
     struct Late {
         u32* p;
         u32 v;
-        u64 at;
+        u64 at;      // op index in the kernel it lands in (controlled), ~0: at that kernel's end
+        u64 issued;  // global op index when it was stored
+        unsigned k_left;
     };
     std::mutex late_m;
-    std::vector<Late> late, landing;
+    std::vector<Late> pending, landing;
     u64 kernel_ops = 0;
-    u64 n_late = 0;
+    std::atomic<u64> gops{0};
+    u64 n_late = 0, n_dropped = 0;
     // the tracked words: every parent[] array of the pipeline (loads elsewhere are never stale)
     std::vector<std::pair<u32*, u32>> arrays;
     std::vector<std::vector<std::vector<u32>>> hist;  // [array][id] -> values since the kernel start (ctl)
     std::vector<std::vector<u32>> start;              // [array][id] -> value at the kernel start (free)
+    std::vector<std::vector<u64>> last_atomic;        // [array][id] -> global op of the last atomic write
 
+    void reset_run() {
+        pending.clear();
+        landing.clear();
+        last_atomic.assign(arrays.size(), {});
+        for (size_t a = 0; a < arrays.size(); ++a) last_atomic[a].assign(arrays[a].second, 0);
+    }
     bool locate(const u32* p, size_t& a, size_t& i) const {
         for (a = 0; a < arrays.size(); ++a)
             if (p >= arrays[a].first && p < arrays[a].first + arrays[a].second) {
@@ -139,15 +160,28 @@ struct Model : gcc::ReplayHooks {
         return false;
     }
     void land(const Late& l) {
-        __atomic_store_n(l.p, l.v, __ATOMIC_RELAXED);
         size_t a, i;
-        if (controlled && locate(l.p, a, i)) hist[a][i].push_back(l.v);
+        if (!locate(l.p, a, i)) return;
+        if (!late_any && __atomic_load_n(&last_atomic[a][i], __ATOMIC_RELAXED) > l.issued) {
+            ++n_dropped;  // an atomic wrote the word after this store was issued: ordered after it
+            return;
+        }
+        __atomic_store_n(l.p, l.v, __ATOMIC_RELAXED);
+        if (controlled) hist[a][i].push_back(l.v);
     }
     void kernel_begin() {
-        landing.swap(late);
-        late.clear();
+        landing.clear();
+        std::vector<Late> keep;
+        for (auto& l : pending) {
+            if (--l.k_left == 0) {
+                l.at = controlled ? splitmix(sched.rng) % 4096 : ~0ull;
+                landing.push_back(l);
+            } else {
+                keep.push_back(l);
+            }
+        }
+        pending.swap(keep);
         kernel_ops = 0;
-        for (auto& l : landing) l.at = controlled ? splitmix(sched.rng) % 4096 : ~0ull;
         hist.resize(arrays.size());
         start.resize(arrays.size());
         for (size_t a = 0; a < arrays.size(); ++a) {
@@ -162,6 +196,7 @@ struct Model : gcc::ReplayHooks {
         }
     }
     void before(const u32*) override {
+        gops.fetch_add(1, std::memory_order_relaxed);
         if (controlled) {
             sched.yield();
             ++kernel_ops;  // serialised by the scheduler
@@ -173,11 +208,16 @@ struct Model : gcc::ReplayHooks {
         if (!late_pm || (splitmix(t_rng) % 1000) >= late_pm) return;
         size_t a, i;
         if (!locate(p, a, i)) return;
+        const unsigned d = 1 + (unsigned)(splitmix(t_rng) % (late_depth ? late_depth : 1));
         std::lock_guard<std::mutex> g(late_m);
-        late.push_back({p, v, 0});
+        pending.push_back({p, v, 0, gops.load(std::memory_order_relaxed), d});
         ++n_late;
     }
-    // the end of a kernel: the late stores of the previous kernel that have not landed yet land now
+    void atomic(const u32* p) override {
+        size_t a, i;
+        if (locate(p, a, i)) __atomic_store_n(&last_atomic[a][i], gops.load(std::memory_order_relaxed), __ATOMIC_RELAXED);
+    }
+    // the end of a kernel: the late stores due in it that have not landed yet land now
     void kernel_end() {
         for (auto& l : landing)
             if (l.at > kernel_ops) land(l);
@@ -223,11 +263,6 @@ struct Model : gcc::ReplayHooks {
             sched.cv.notify_all();
         }
         for (auto& x : th) x.join();
-        kernel_end();
-    }
-    // host work between kernels that swaps or rereads arrays: whatever is still in flight lands first
-    void drain() {
-        kernel_begin();
         kernel_end();
     }
 };
@@ -308,15 +343,38 @@ static void k_fold(Forest& f, const Edge* e, u64 n, int T, u64 seed, int rec) {
     });
 }
 
-// compress_kernel: labels into the spare buffer, then swap
+// compress_bits_kernel: labels into the spare buffer (plain stores, through the late-store model), then swap. SPLIT:
+// its finds split paths in the old buffer (plain stores there too; round 4's product), else read-only finds (round 5)
+template <bool SPLIT>
 static void k_compress_out(Forest& f, int T, u64 seed) {
     u32* par = f.parent.data();
     u32* lab = f.spare.data();
     const u32 V = f.V;
     g_model.kernel(T, seed, [&](int t) {
-        for (u32 v = (u32)t; v < V; v += (u32)T) lab[v] = gcc::compress_label(par, v);
+        gcc::NoCount c;
+        for (u32 v = (u32)t; v < V; v += (u32)T) {
+            const u32 p = gcc::ld(&par[v]);
+            const u32 l = p >= v ? p : gcc::UnionFind<gcc::LoadPlain, SPLIT>::find_from(par, v, p, c);
+            gcc::st(&lab[v], l);
+        }
     });
     std::swap(f.parent, f.spare);
+    f.rec_all = false;
+}
+static bool g_compress_split = false;  // the product's full compress: split (round 4) or read-only finds (round 5)
+static void k_compress_out(Forest& f, int T, u64 seed) {
+    if (g_compress_split) k_compress_out<true>(f, T, seed);
+    else k_compress_out<false>(f, T, seed);
+}
+
+// bucket_init_kernel / seed_pack_kernel<true>: parent[v] := v in C ? g : UNSEEN with plain stores (the reset and
+// every union inside C in one write); the filtered / bucketed passes then hook with memory-side atomics
+static void k_init(Forest& f, const std::vector<char>& inC, u32 g, int T, u64 seed) {
+    u32* par = f.parent.data();
+    const u32 V = f.V;
+    g_model.kernel(T, seed, [&](int t) {
+        for (u32 v = (u32)t; v < V; v += (u32)T) gcc::st(&par[v], inC[v] ? g : U);
+    });
     f.rec_all = false;
 }
 
@@ -339,7 +397,8 @@ static void k_compress_inplace(Forest& f, int T, u64 seed) {
 
 // compress_inc_kernel<true>: the bloom is the kernel's LDS copy (taken at its start); 4 consecutive ids per lane
 // read before any of them is labelled (the 16-B load), only changed slots written; the other bloom is cleared.
-static void k_compress_inc_inplace(Forest& f, int T, u64 seed) {
+// through: the labels written write-through (gcc::st_through, round 5's product) or with plain stores (rounds 3-4)
+static void k_compress_inc_inplace(Forest& f, int T, u64 seed, bool through) {
     u32* par = f.parent.data();
     const std::vector<u32> lds = f.bloom[f.bloom_cur];
     const u32 V = f.V;
@@ -354,7 +413,10 @@ static void k_compress_inc_inplace(Forest& f, int T, u64 seed) {
                     if (p[k] < v0 + k && gcc::bloom_test(lds.data(), p[k]))
                         n_inc_finds.fetch_add(1, std::memory_order_relaxed);
                     lab[k] = gcc::inc_label(par, lds.data(), v0 + k, p[k]);
-                    if (lab[k] != p[k]) gcc::st(&par[v0 + k], lab[k]);
+                    if (lab[k] != p[k]) {
+                        if (through) gcc::st_through(&par[v0 + k], lab[k]);
+                        else gcc::st(&par[v0 + k], lab[k]);
+                    }
                 }
         }
     });
@@ -362,9 +424,9 @@ static void k_compress_inc_inplace(Forest& f, int T, u64 seed) {
 }
 
 // the product's compress_now: incremental in place when every mutation since the last compress was recorded
-static void compress_product_inc(Forest& f, int T, u64 seed) {
+static void compress_product_inc(Forest& f, int T, u64 seed, bool through = true) {
     if (f.rec_all) {
-        k_compress_inc_inplace(f, T, seed);
+        k_compress_inc_inplace(f, T, seed, through);
     } else {
         k_compress_out(f, T, seed);
         std::fill(f.bloom[f.bloom_cur ^ 1].begin(), f.bloom[f.bloom_cur ^ 1].end(), 0u);
@@ -474,11 +536,10 @@ static void chain_of(const std::vector<u32>& par, u32 v, std::vector<u32>& out) 
 
 static int run(const std::string& pipe, u32 V, const std::vector<u64>& wstart, const std::vector<Edge>& E, int T,
                u64 seed, std::vector<u32>& bad_windows, Failure& first) {
-    g_model.late.clear();  // late stores of an earlier run point into its freed forest
-    g_model.landing.clear();
     Forest f(V);
     SeqUF ref(V), peer(V);
     g_model.arrays = {{f.parent.data(), V}, {f.spare.data(), V}};
+    g_model.reset_run();  // late stores of an earlier run point into its freed forest
     std::vector<char> inT(V, 0);
     u32 g = U;
     int bad = 0;
@@ -498,8 +559,33 @@ static int run(const std::string& pipe, u32 V, const std::vector<u64>& wstart, c
             k_fold(f, e, n, T, ks + 1, false);
             k_compress_inplace<false>(f, T, ks + 2);
         } else if (pipe == "inc" || pipe == "inc_split") {
+            // inc_split is round 3's product as it was: the recording fold with path splitting AND plain label stores
+            // in the in-place compress
             k_fold(f, e, n, T, ks + 1, pipe == "inc" ? 1 : 2);
-            compress_product_inc(f, T, ks + 2);
+            compress_product_inc(f, T, ks + 2, pipe == "inc");
+        } else if (pipe == "init") {
+            // a fresh forest's seeded / bucketed start: C = the component of the window's most frequent endpoint
+            // among its own edges (any set inside one component of the batch is a valid seed), g = min C, one plain
+            // store per id, then the filtered fold against C; later windows as "filter"
+            if (g == U) {
+                SeqUF s(V);
+                std::vector<u32> deg(V, 0);
+                for (u64 i = 0; i < n; ++i) s.unite(e[i].a, e[i].b), ++deg[e[i].a], ++deg[e[i].b];
+                u32 h = 0;
+                for (u32 v = 1; v < V; ++v)
+                    if (deg[v] > deg[h]) h = v;
+                const u32 rh = s.find(h);
+                g = U;
+                for (u32 v = 0; v < V; ++v) {
+                    inT[v] = s.p[v] != U && s.find(v) == rh;
+                    if (inT[v] && g == U) g = v;
+                }
+                k_init(f, inT, g, T, ks + 1);
+            }
+            k_filtered(f, e, n, inT, g, T, ks + 3, 2, 2);
+            k_compress_out(f, T, ks + 2);
+            g = giant_of(f.parent);
+            for (u32 v = 0; v < V; ++v) inT[v] = g != U && f.parent[v] == g;
         } else if (pipe == "filter") {
             if (g == U) k_fold(f, e, n, T, ks + 1, false);  // the first window: nothing tracked yet
             else k_filtered(f, e, n, inT, g, T, ks + 1, 2, 2);
@@ -576,6 +662,9 @@ int main(int argc, char** argv) {
     const int seeds = std::atoi(argv[4]);
     g_model.stale_pm = (unsigned)std::atoi(argv[5]);
     g_model.late_pm = argc > 6 ? (unsigned)std::atoi(argv[6]) : 0;
+    g_model.late_depth = argc > 7 ? (unsigned)std::atoi(argv[7]) : 1;
+    g_model.late_any = argc > 8 ? std::string(argv[8]) != "plain" : true;
+    g_compress_split = argc > 9 ? std::string(argv[9]) == "split" : false;
     u32 V, W;
     if (std::scanf("%u %u", &V, &W) != 2) return 1;
     std::vector<u64> ws(W + 1, 0);
@@ -619,10 +708,10 @@ int main(int argc, char** argv) {
     }
     gcc::replay = nullptr;
     std::printf("pipeline=%s mode=%s threads=%d runs=%d bad_runs=%d bad_windows=%llu hooks=%llu hook_unions=%llu "
-                "absorb_stores=%llu inc_finds=%llu late_stores=%llu\n",
+                "absorb_stores=%llu inc_finds=%llu late_stores=%llu late_dropped=%llu\n",
                 pipe.c_str(), mode.c_str(), T, seeds, bad_runs, (unsigned long long)bad_windows,
                 (unsigned long long)n_hooks.load(), (unsigned long long)n_hook_unions.load(),
                 (unsigned long long)n_absorb_stores.load(), (unsigned long long)n_inc_finds.load(),
-                (unsigned long long)g_model.n_late);
+                (unsigned long long)g_model.n_late, (unsigned long long)g_model.n_dropped);
     return 0;
 }

@@ -221,7 +221,7 @@ def test_giant_fold_knobs_and_no_dominant_component():
     c.close()
 
 
-def _bip_group_worker(rank, world, port, pairs, starts, q):
+def _bip_group_worker(rank, world, port, pairs, starts, q, extra_ids=0):
     """One rank (spawned before any GPU call): folds its contiguous 1/world of every window into a Candidates on
     cuda:0, then bipartite.merge_group over gloo; reports (success, words) per window."""
     import sys
@@ -238,7 +238,7 @@ def _bip_group_worker(rank, world, port, pairs, starts, q):
         from gelly_stream.bipartite import Candidates as C
         from gelly_stream.bipartite import merge_group
 
-        V = int(pairs.max()) + 1
+        V = int(pairs.max()) + 1 + (extra_ids if rank == 1 else 0)
         d = torch.from_numpy(pairs.reshape(-1).view(np.int32)).cuda()
         c = C(V)
         out = []
@@ -299,3 +299,46 @@ def test_merge_group_two_ranks_share_one_gpu(odd):
             assert ok == bool(want["success"][w]), (r, w)
             if ok:
                 assert np.array_equal(words, want["words"][w]), (r, w)
+
+
+def test_merge_group_rejects_different_id_ranges():
+    """the ranks' id_capacity is checked (all_reduce MAX of +cap and -cap beside the fail flag) before any
+    words move: a rank with a larger id range makes merge_group raise on EVERY rank, instead of a mismatched
+    all_gather."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    pairs = np.asarray([[0, 1], [2, 3], [4, 5], [6, 7]], dtype=np.uint32)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bip_group_worker, args=(r, 2, port, pairs, [0, 4], q, 64)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        results = dict(q.get(timeout=150) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(2):
+        assert isinstance(results[r], str) and "id_capacity differ" in results[r], results
+
+
+def test_device_words_tensor_matches_host_words():
+    """The send side of merge_group over nccl: the canonical words straight from the forest's device buffer
+    (gcc_signed_device_words wrapped through __cuda_array_interface__) equal the host copy."""
+    cfg = G.scaled(G.CONFIGS["c4_kron26"], scale=14, n_edges=1 << 16)
+    E, V = cfg.info()
+    pairs = G.to_bipartite(G.generate_host(cfg))
+    c = Candidates(V)
+    c.fold(pairs)
+    t = c.device_words_tensor()
+    assert t.device.type == "cuda" and t.dtype.itemsize == 4 and t.numel() == V
+    assert np.array_equal(t.cpu().numpy().view(np.uint32), c.words())
+    c.close()
