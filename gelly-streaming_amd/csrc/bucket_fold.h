@@ -362,7 +362,7 @@ template <int P1B, int P1P, u32 MAXB = 256, u32 W = 4>
 __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                           Meta* __restrict__ m, u32* __restrict__ bk_lo,
                                                           u16* __restrict__ bk_hi, u64* __restrict__ ovf, u32 ovf_cap,
-                                                          u32* __restrict__ err) {
+                                                          u32* __restrict__ err, u32* __restrict__ reset) {
     trace_start(kTrBkP1);
     // the tile in bucket order: dynamic LDS (p1_lds: P1B * P1P + 3 MAXB u64, 66 / 130 KiB), set up like every
     // kernel's LDS beyond 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-bucket state below is static (MAXB >= ns)
@@ -391,6 +391,11 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
     const u64 n2 = n / 2;                                  // whole pairs
     const u64 ntiles = (n2 * 2 + (P1B * P1P) - 1) / (P1B * P1P);
     constexpr int kQ = P1P / 2;
+    // reset (round 5): a fresh forest's lazy reset, parent[] := UNSEEN, spread over the tiles: tile t stores its
+    // 1/ntiles of the id range behind the next tile's loads (P1 never reads parent[]; the waves mostly wait for their
+    // loads). It replaces bucket_init_kernel's 4 B per id of its own launch: C is deferred like N (bucket_join_kernel)
+    const u64 rq = reset ? (u64)cap / 4 : 0;  // whole 16-B quads; the last cap % 4 ids here:
+    if (reset && blockIdx.x == 0 && threadIdx.x < (cap & 3u)) reset[4 * rq + threadIdx.x] = GCC_UNSEEN_DEV;
     if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) {  // the odd last edge
         u32 a = (u32)edges[n - 1], b = (u32)(edges[n - 1] >> 32);
         if (edge_ok(a, b, cap, err)) {
@@ -426,6 +431,11 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
             ok[2 * k] = ok[2 * k + 1] = j < n2;
         }
         if (t + gridDim.x < ntiles) load_tile(t + gridDim.x, q);  // the next tile streams in meanwhile
+        if (reset) {
+            const u4 un = {GCC_UNSEEN_DEV, GCC_UNSEEN_DEV, GCC_UNSEEN_DEV, GCC_UNSEEN_DEV};
+            for (u64 x = rq * t / ntiles + threadIdx.x; x < rq * (t + 1) / ntiles; x += P1B)
+                reinterpret_cast<u4*>(reset)[x] = un;
+        }
         GCC_PH_MARK(phc, 0);  // waited for this tile's loads
 #pragma unroll
         for (int k = 0; k < P1P; ++k) {
@@ -964,16 +974,26 @@ __global__ __launch_bounds__(kBlock) void bucket_hook_kernel(u32* __restrict__ p
 // id of N directly; only FINAL P2's in-kernel ring unions (a full slow region, m->ring_used) could have made one
 // seen, and then every seen id of N is hooked under g here. later (a later window, round 4): ids of N may be seen
 // already, members of other components: every seen id of N is hooked under g here, only the new ones are deferred.
+// defer_c (a fresh forest, round 5): C itself is deferred the same way — P1 reset parent[] to UNSEEN and no kernel
+// stored g into C's slots (bucket_init_kernel's job until round 4), so nbits := C | N here, for the closing compress,
+// and with ring_used the seen ids of C are hooked too (a ring union may have made one seen, under another root).
 __global__ __launch_bounds__(kBlock) void bucket_join_kernel(u32* __restrict__ parent, u32* __restrict__ bits,
-                                                             const u32* __restrict__ nbits, u32 nwords32,
+                                                             u32* __restrict__ nbits, u32 nwords32,
                                                              const u32* __restrict__ giant, const Meta* __restrict__ m,
-                                                             u32 later) {
+                                                             u32 later, u32 defer_c) {
     trace_start(kTrBkHook);
     const u32 g = *giant;
     const bool ring = m->ring_used != 0 || later;
     for (u64 w = (u64)blockIdx.x * kBlock + threadIdx.x; w < nwords32; w += (u64)gridDim.x * kBlock) {
         u32 d = nbits[w];
-        if (!d) continue;
+        const u32 cw = defer_c ? bits[w] : 0u;
+        if (defer_c) {
+            if (!(d | cw)) continue;
+            if (~d & cw) nbits[w] = d | cw;
+            if (ring) d |= cw;  // the seen ids of C too
+        } else if (!d) {
+            continue;
+        }
         bits[w] |= d;
         if (g == GCC_UNSEEN_DEV) continue;
         // an id below g is hooked now: it becomes the component's root, which the compress must find
@@ -1036,8 +1056,14 @@ __global__ __launch_bounds__(kHubBlock) void bucket_hub_kernel(const u64* __rest
     }
 }
 
+// giant := g = min C, the component's representative (a fresh forest whose C is deferred: P1 did the reset).
+__global__ void bucket_root_kernel(const Meta* __restrict__ m, u32* __restrict__ giant) {
+    trace_start(kTrBkInit);
+    *giant = m->gmin;
+}
+
 // parent[v] := v in C ? g : UNSEEN over the whole id range (the reset and all of C's unions in one write);
-// giant := g. 4 ids per lane, 16-B stores.
+// giant := g. 4 ids per lane, 16-B stores. (With bucket_defer: P1's reset + bucket_root_kernel instead.)
 __global__ __launch_bounds__(kBlock) void bucket_init_kernel(u32* __restrict__ parent, u32 n,
                                                              const u32* __restrict__ bits, const Meta* __restrict__ m,
                                                              u32* __restrict__ giant) {

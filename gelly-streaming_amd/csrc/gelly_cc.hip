@@ -2497,25 +2497,29 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u32 cps_seed_v = std::max<u32>(1, cps_seed * ns / nvs / vratio);
     const size_t vl_cur_off = offsetof(bk::Meta, vl_cur);
     u32 slot = 0;
+    // a fresh forest with the deferred N: C is deferred too (round 5), and P1 performs the lazy reset itself
+    const bool defer = t.bucket_defer != 0;
+    const bool defer_c = fresh && defer;
+    u32* p1_reset = defer_c ? h->d_parent : nullptr;
     rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta,
                   p1_blocks, p2_blocks, chunk);
     if (!rc)
         rc = ns > 256  // beyond 2^27 ids: 512 buckets' state and the 16K-edge tile exceed the LDS; 12K-edge tiles
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 12, 512>, dim3(h->n_cu), dim3(1024),
                             bk::p1_lds(1024, 12, 512), edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap,
-                            h->d_err)
+                            h->d_err, p1_reset)
              : t.bucket_p1 == 1
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16>, dim3(h->n_cu), dim3(1024), bk::p1_lds(1024, 16),
-                            edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err)
+                            edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err, p1_reset)
              : t.bucket_p1 == 3
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 16, 256, 8>, dim3(h->n_cu), dim3(1024),
                             bk::p1_lds(1024, 16, 256, 8), edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap,
-                            h->d_err)
+                            h->d_err, p1_reset)
              : t.bucket_p1 == 2
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 12>, dim3(h->n_cu), dim3(1024), bk::p1_lds(1024, 12),
-                            edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err)
+                            edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err, p1_reset)
                  : launch_k(h, "bucket", n, bk::bucket_kernel<512, 16>, dim3(p1_blocks), dim3(512), bk::p1_lds(512, 16),
-                            edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err);
+                            edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err, p1_reset);
     if (rc) return rc;
     // seeding (a fresh forest): C := {hub}, then levels over the sample. A later window keeps C = the tracked
     // component's bitmap and its root (the last compress wrote both), and parent[] as it is.
@@ -2538,10 +2542,13 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
             rc = launch_k(h, "seed_hook", 0, bk::slice_hook_kernel<false>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
                           bits, nw32, nvs, h->d_meta, vl, cps_seed_v, slot++, h->cap, h->d_err);
     }
-    // parent[] := C ? g : UNSEEN (the reset), then every bucketed edge, the overflow list, a spill
+    // parent[] := C ? g : UNSEEN (the reset), then every bucketed edge, the overflow list, a spill. With C deferred,
+    // P1 did the reset and only g is published here
     if (!rc && fresh)
-        rc = launch_k(h, "bucket_init", 0, bk::bucket_init_kernel, dim3(grid_for(((u64)h->cap + 3) / 4, kMaxGrid)),
-                      dim3(kBlock), 0, h->d_parent, h->cap, (const u32*)bits, (const bk::Meta*)h->d_meta, giant);
+        rc = defer_c ? launch_k(h, "bucket_init", 0, bk::bucket_root_kernel, dim3(1), dim3(1), 0,
+                                (const bk::Meta*)h->d_meta, giant)
+                     : launch_k(h, "bucket_init", 0, bk::bucket_init_kernel, dim3(grid_for(((u64)h->cap + 3) / 4, kMaxGrid)),
+                                dim3(kBlock), 0, h->d_parent, h->cap, (const u32*)bits, (const bk::Meta*)h->d_meta, giant);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, nvs * sizeof(u32), h->stream));
 #define GCC_P2_FINAL(PER, VW)                                                                                      \
@@ -2564,11 +2571,10 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
                       h->d_nbits, nw32, nvs, h->d_meta, vl, cps_v, slot++, h->cap, h->d_err);
-    const bool defer = t.bucket_defer != 0;
     if (!rc)
         rc = defer ? launch_k(h, "bucket_join", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
-                              h->d_parent, bits, (const u32*)h->d_nbits, nw32, (const u32*)giant, (const bk::Meta*)h->d_meta,
-                              (u32)!fresh)
+                              h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant, (const bk::Meta*)h->d_meta,
+                              (u32)!fresh, (u32)defer_c)
                    : launch_k(h, "bucket_hook", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
                               h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
     // Second level over the slow edges, now against C | N: a slow edge whose source joined N is a hook of its
@@ -2590,8 +2596,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                           h->d_nbits, nw32, nvs, h->d_meta, vl, cps_v, slot++, h->cap, h->d_err);
         if (!rc)
             rc = defer ? launch_k(h, "bucket_join2", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock),
-                                  0, h->d_parent, bits, (const u32*)h->d_nbits, nw32, (const u32*)giant,
-                                  (const bk::Meta*)h->d_meta, (u32)!fresh)
+                                  0, h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant,
+                                  (const bk::Meta*)h->d_meta, (u32)!fresh, (u32)defer_c)
                        : launch_k(h, "bucket_hook2", 0, bk::bucket_hook_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock),
                                   0, h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant);
         slow_list = reinterpret_cast<const u64*>(h->d_bk);

@@ -177,8 +177,8 @@ class Candidates:
         call("gcc_signed_device_words", self.handle, byref(p))
         self.getSuccess()  # synchronises the forest's stream: the compress has written the words
 
-        class _View:  # __cuda_array_interface__ over the forest's buffer (read-only, valid until its next mutation)
-            __cuda_array_interface__ = {"shape": (self.id_capacity,), "typestr": "<i4", "data": (p.value, True),
+        class _View:  # __cuda_array_interface__ over the forest's buffer (copied at once: valid until its next mutation)
+            __cuda_array_interface__ = {"shape": (self.id_capacity,), "typestr": "<i4", "data": (p.value, False),
                                         "version": 2, "strides": None}
 
         with torch.cuda.device(self.device):
