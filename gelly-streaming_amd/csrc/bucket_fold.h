@@ -60,7 +60,9 @@ struct Meta {
     u32 bk_cur[kMaxBuckets];   // reservation cursor (may pass bk_cap: the rest went to the overflow list)
     u64 vl_base[kMaxVLists];   // v-list s (targets in slice s): entries [vl_base[s], vl_base[s] + vl_cap[s])
     u32 vl_cap[kMaxVLists];
-    u32 vl_cur[kMaxVLists];    // may pass vl_cap: those v's were hooked inline (FINAL) or dropped (SEED)
+    // per pass (seeding levels, FINAL, the second level: kVlPasses), may pass vl_cap: those v's were hooked inline
+    // (FINAL) or dropped (SEED). One array per pass, all zeroed by the layout (round 5: no memset between passes)
+    u32 vl_cur[8][kMaxVLists];
     u32 work[16];                // per-launch dequeue counters
     u32 ovf_cur;                 // overflow list cursor (may pass its capacity: then `spill`)
     u32 spill;                   // 1: some edge fit neither its bucket nor the overflow list
@@ -69,7 +71,14 @@ struct Meta {
     u32 ring_used;               // FINAL P2 united some slow edges itself (its region was full): see bucket_join_kernel
     u32 chunk;                   // entries per chunk reservation (chunk_entries)
     u32 slow_cnt[kMaxP2Blocks];  // FINAL P2: slow edges (source not in C) each block listed in its own region
+    // the layout's sample counts, summed over its blocks; its last block reads them with atomicExch(0), so they are
+    // zero again for the next layout (zeroed once when Meta is allocated)
+    u32 lay_cu[kMaxBuckets];
+    u32 lay_cv[kMaxVLists];
+    u32 lay_done;
 };
+constexpr u32 kVlPasses = 8;  // Meta::vl_cur: seeding levels 0..5, FINAL (6), the second level (7)
+constexpr u32 kVlFinal = 6, kVlLevel2 = 7;
 
 // A run of one P2 block's slow list whose edges share a source slice (one P2 item's slow edges): the second
 // filter level (slice_filter_kernel<true, true>) takes these runs as its items. off is even (runs padded to pairs).
@@ -254,40 +263,66 @@ __device__ __forceinline__ void block_prefix(const u32* cap, u64* base, u32 ns, 
     __syncthreads();
 }
 
+// Round 5: kLayoutBlocks blocks, each counting its runs of the sample in LDS and adding the counts to Meta::lay_*; the
+// block that arrives last (a ticket) computes the capacities and prefix sums (one 1024-thread block took 22 us per
+// fresh fold for the whole sample: C4 in 8 windows 0.18 ms per step). A fresh fold also clears C's bitmap here (every
+// block its share; it was a memset) and the last block elects the hub (bucket_hub_kernel until round 4): C := {h},
+// gmin := h. dynamic LDS: 2 x kHubSlots u32 when elect, else none.
+constexpr u32 kLayoutBlocks = 64;
 __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                               Meta* __restrict__ m, u32 bk_blocks, u32 vl_blocks,
-                                                              u32 chunk) {
+                                                              u32 chunk, u32* __restrict__ bits_clear, u32 nwords32,
+                                                              u32 elect) {
     trace_start(kTrBkLayout);
+    extern __shared__ __attribute__((aligned(16))) u32 s_tab[];  // the hub election's table (elect only)
     __shared__ u32 s_cu[kMaxBuckets], s_cv[kMaxVLists];
     __shared__ u64 s_scan[1024];
+    __shared__ u32 s_last;
     const u32 nvs = vslices(cap);
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
         s_cu[s] = 0;
         if (s < nvs) s_cv[s] = 0;
     }
+    if (bits_clear) {  // 16-B stores; nwords32 is even (host: 2 x 64-bit words)
+        typedef u32 u4 __attribute__((ext_vector_type(4)));
+        const u4 z = {0u, 0u, 0u, 0u};
+        for (u32 w = 4 * (blockIdx.x * 1024 + threadIdx.x); w < nwords32; w += 4 * gridDim.x * 1024) {
+            if (w + 3 < nwords32) *reinterpret_cast<u4*>(bits_clear + w) = z;
+            else
+                for (u32 k = w; k < nwords32; ++k) bits_clear[k] = 0u;
+        }
+    }
     __syncthreads();
     const u64 n_smp = n < kSample ? n : kSample;
     // the sample: kSample / 1024 = 64 runs of 1024 CONSECUTIVE edges spread evenly over the batch (coalesced, 64
-    // pages; single edges kSample apart touched 64K pages and took this one block 0.12 ms on C4), 32 loads in
-    // flight per thread (64 would spill)
-    constexpr u32 kPer = kSample / 1024, kBatch = 32;
+    // pages; single edges kSample apart touched 64K pages), one run per block
+    constexpr u32 kPer = kSample / 1024;
     const u64 run_stride = n / kPer;  // >= 1024 whenever n >= kSample; below that the sample is the batch
-    for (u32 b = 0; b < kPer; b += kBatch) {
-        u64 e[kBatch];
-#pragma unroll
-        for (u32 i = 0; i < kBatch; ++i) {
-            const u64 k = n <= kSample ? threadIdx.x + (u64)(b + i) * 1024 : (u64)(b + i) * run_stride + threadIdx.x;
-            e[i] = k < n ? edges[k] : ~0ull;
-        }
-#pragma unroll
-        for (u32 i = 0; i < kBatch; ++i) {
-            const u32 u = (u32)e[i], v = (u32)(e[i] >> 32);
-            if (u < cap && v < cap) {
-                atomicAdd(&s_cu[u >> kSliceBits], 1u);
-                atomicAdd(&s_cv[v >> kVSliceBits], 1u);
-            }
+    for (u32 b = blockIdx.x; b < kPer; b += gridDim.x) {
+        const u64 k = n <= kSample ? threadIdx.x + (u64)b * 1024 : (u64)b * run_stride + threadIdx.x;
+        const u64 e = k < n ? edges[k] : ~0ull;
+        const u32 u = (u32)e, v = (u32)(e >> 32);
+        if (u < cap && v < cap) {
+            atomicAdd(&s_cu[u >> kSliceBits], 1u);
+            atomicAdd(&s_cv[v >> kVSliceBits], 1u);
         }
     }
+    __syncthreads();
+    for (u32 s = threadIdx.x; s < ns; s += 1024) {
+        if (s_cu[s]) atomicAdd(&m->lay_cu[s], s_cu[s]);
+        if (s < nvs && s_cv[s]) atomicAdd(&m->lay_cv[s], s_cv[s]);
+    }
+    __threadfence();  // release: this block's counts and bitmap zeros before its ticket
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&m->lay_done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // acquire: every block's counts
+    for (u32 s = threadIdx.x; s < ns; s += 1024) {
+        s_cu[s] = atomicExch(&m->lay_cu[s], 0u);  // the total, and zero for the next layout
+        if (s < nvs) s_cv[s] = atomicExch(&m->lay_cv[s], 0u);
+    }
+    if (threadIdx.x == 0) atomicExch(&m->lay_done, 0u);
     __syncthreads();
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
         m->bk_cap[s] = est_cap(s_cu[s], n, n_smp, bk_blocks, chunk);
@@ -295,7 +330,8 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
         m->bk_cur[s] = 0;
         if (s < nvs) {
             m->vl_cap[s] = est_cap(s_cv[s], n, n_smp, vl_blocks, chunk);
-            m->vl_cur[s] = 0;
+#pragma unroll
+            for (u32 p = 0; p < kVlPasses; ++p) m->vl_cur[p][s] = 0;
         }
     }
     __syncthreads();
@@ -308,6 +344,15 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     if (threadIdx.x == 0) {
         m->ovf_cur = 0;
         m->spill = 0;
+    }
+    if (elect) {  // the seeding's hub: the deterministic election of the seeded fold over the batch's first edges
+        u64 e[kHubPer];
+        hub_sample(edges, n < kHubSample ? n : kHubSample, e);
+        const u32 h = hub_elect(e, s_tab, cap);
+        if (threadIdx.x == 0) {
+            m->gmin = h;
+            if (h != GCC_UNSEEN_DEV) atomicOr(&bits_clear[h >> 5], 1u << (h & 31));  // after every block's zeros
+        }
     }
 }
 
@@ -560,7 +605,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                                                                 u32 frac, u32 work_slot, u32 drain_at, u32 hub_only,
                                                                 const u32* __restrict__ giant, u64* __restrict__ slow,
                                                                 u32 slow_cap, u32 cap, u32* __restrict__ err,
-                                                                SlowSeg* __restrict__ segs) {
+                                                                SlowSeg* __restrict__ segs, u32 pass) {
     static_assert(FINAL || !SEG, "the second level is a FINAL pass");
     trace_start(FINAL ? kTrBkP2 : kTrBkP2Seed);
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
@@ -786,7 +831,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
             // the reservations (their global atomics) overlap the other waves' scatter
             for (u32 s = threadIdx.x; s < nvs; s += kP2Block) {
                 const u32 pc = padw<VW>(s_cnt[s]);
-                if (pc) reserve_run(runs, s, pc, &m->vl_cur[s], s_vcap[s], chunk);
+                if (pc) reserve_run(runs, s, pc, &m->vl_cur[pass][s], s_vcap[s], chunk);
                 for (u32 j = s_cnt[s]; j < pc; ++j) s_vt[s_start[s] + j] = 0xFFFFFFFFu;
             }
 #pragma unroll
@@ -863,7 +908,7 @@ template <bool FINAL>
 __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ bits, u32* __restrict__ out,
                                                               u32 nwords32, u32 ns, Meta* __restrict__ m,
                                                               VList vl, u32 cps, u32 work_slot,
-                                                              u32 cap, u32* __restrict__ err) {
+                                                              u32 cap, u32* __restrict__ err, u32 pass) {
     trace_start(FINAL ? kTrBkP3 : kTrBkP3Seed);
     extern __shared__ __attribute__((aligned(16))) u32 s_bits[];  // kVSliceWords
     __shared__ u32 s_item, s_min;
@@ -891,7 +936,7 @@ __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ 
         const u32 item = s_item;
         if (item >= n_items) break;
         const u32 sl = item / cps;
-        const u64 len = m->vl_cur[sl] < m->vl_cap[sl] ? m->vl_cur[sl] : m->vl_cap[sl];
+        const u64 len = m->vl_cur[pass][sl] < m->vl_cap[sl] ? m->vl_cur[pass][sl] : m->vl_cap[sl];
         u64 lo, hi;
         item_range(len, item % cps, cps, lo, hi);
         if (lo >= hi) continue;
@@ -1038,21 +1083,6 @@ __global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ p
         if (ia) hook_g(parent, g, b);
         else if (ib) hook_g(parent, g, a);
         else UF::unite(parent, a, b, c);
-    }
-}
-
-// Seeding start: clear the bitmap (done by the host's memset), elect the hub h of the batch's first edges (the
-// same deterministic election as the seeded fold), C := {h}, gmin := h. One block.
-__global__ __launch_bounds__(kHubBlock) void bucket_hub_kernel(const u64* __restrict__ edges, u64 n, u32 cap,
-                                                               u32* __restrict__ bits, Meta* __restrict__ m) {
-    trace_start(kTrBkHub);
-    extern __shared__ __attribute__((aligned(16))) u32 s_tab[];
-    u64 e[kHubPer];
-    hub_sample(edges, n < kHubSample ? n : kHubSample, e);
-    const u32 h = hub_elect(e, s_tab, cap);
-    if (threadIdx.x == 0) {
-        m->gmin = h;
-        if (h != GCC_UNSEEN_DEV) bits[h >> 5] = 1u << (h & 31);
     }
 }
 

@@ -1805,6 +1805,8 @@ struct FoldTune {
     double bucket_hub_sample = 1.0;  // the first level's share of the hub's bucket (C = {h}: one slice)
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
     int bucket_defer = 1;        // N labelled by the fold's closing compress instead of a store per id (bucket_join_kernel)
+    // a fresh forest's C deferred like N, the reset done by P1 (round 5) instead of bucket_init_kernel's 4 B per id
+    int bucket_defer_c = 1;
     int bucket_slow2 = 1;        // second filter level over the slow edges with C | N (C4's 1/8 share: 19 % slow edges)
     int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms), 2 = 1024 x 12,
                                  // 3 = 1024 x 16 with 8-entry write-out lanes (16-B hi stores)
@@ -2447,6 +2449,9 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (!h->d_meta) {
         HIP_TRY(hipMalloc((void**)&h->d_meta, sizeof(bk::Meta)));
         if (poison_scratch()) HIP_TRY(hipMemsetAsync(h->d_meta, 0xA5, sizeof(bk::Meta), h->stream));
+        // the layout's sample counters start at zero (its last block leaves them zero)
+        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + offsetof(bk::Meta, lay_cu), 0,
+                               sizeof(bk::Meta) - offsetof(bk::Meta, lay_cu), h->stream));
     }
     const u32 p1_blocks = 2 * (u32)h->n_cu;  // (bucket_p1 = 1 runs n_cu blocks: fewer writers, same slack bound)
     const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
@@ -2495,14 +2500,15 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u32 vratio = 1u << (bk::kVSliceBits - bk::kSliceBits);
     const u32 cps_v = std::max<u32>(1, cps * ns / nvs / vratio);
     const u32 cps_seed_v = std::max<u32>(1, cps_seed * ns / nvs / vratio);
-    const size_t vl_cur_off = offsetof(bk::Meta, vl_cur);
     u32 slot = 0;
     // a fresh forest with the deferred N: C is deferred too (round 5), and P1 performs the lazy reset itself
     const bool defer = t.bucket_defer != 0;
-    const bool defer_c = fresh && defer;
+    const bool defer_c = fresh && defer && t.bucket_defer_c;
     u32* p1_reset = defer_c ? h->d_parent : nullptr;
-    rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta,
-                  p1_blocks, p2_blocks, chunk);
+    // the layout (parallel, round 5) also clears C's bitmap and elects the hub of a fresh forest
+    rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(bk::kLayoutBlocks), dim3(1024),
+                  fresh ? 2 * kHubSlots * sizeof(u32) : 0, edges, n, ns, h->cap, h->d_meta, p1_blocks, p2_blocks, chunk,
+                  fresh ? bits : (u32*)nullptr, nw32, (u32)fresh);
     if (!rc)
         rc = ns > 256  // beyond 2^27 ids: 512 buckets' state and the 16K-edge tile exceed the LDS; 12K-edge tiles
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 12, 512>, dim3(h->n_cu), dim3(1024),
@@ -2523,24 +2529,18 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (rc) return rc;
     // seeding (a fresh forest): C := {hub}, then levels over the sample. A later window keeps C = the tracked
     // component's bitmap and its root (the last compress wrote both), and parent[] as it is.
-    if (fresh) {
-        HIP_TRY(hipMemsetAsync(bits, 0, (size_t)nw32 * sizeof(u32), h->stream));
-        rc = launch_k(h, "bucket_hub", 0, bk::bucket_hub_kernel, dim3(1), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32),
-                      edges, n, h->cap, bits, h->d_meta);
-    }
     const u32 frac = (u32)std::max(0.0, std::min(65536.0, t.bucket_sample * 65536.0));
     const u64 sample_edges = (u64)((double)n * frac / 65536.0);
     const int levels = fresh ? std::max(0, std::min(6, t.bucket_levels)) : 0;
     for (int l = 0; l < levels && !rc; ++l) {
-        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, nvs * sizeof(u32), h->stream));
         rc = launch_k(h, "seed_filter", sample_edges, bk::slice_filter_kernel<false>, dim3(p2_blocks), dim3(bk::kP2Block),
                       f_lds, h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,
                       (const u32*)bits, nw32, ns, h->d_meta, vl, l == 0 ? cps_hub : cps_seed, l == 0 ? frac_hub : frac, slot++, h->tune.drain_at, (u32)(l == 0),
                       (const u32*)giant, h->d_slow, slow_cap, h->cap, h->d_err,
-                      (bk::SlowSeg*)nullptr);
+                      (bk::SlowSeg*)nullptr, (u32)l);
         if (!rc)
             rc = launch_k(h, "seed_hook", 0, bk::slice_hook_kernel<false>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                          bits, nw32, nvs, h->d_meta, vl, cps_seed_v, slot++, h->cap, h->d_err);
+                          bits, nw32, nvs, h->d_meta, vl, cps_seed_v, slot++, h->cap, h->d_err, (u32)l);
     }
     // parent[] := C ? g : UNSEEN (the reset), then every bucketed edge, the overflow list, a spill. With C deferred,
     // P1 did the reset and only g is published here
@@ -2550,12 +2550,11 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                      : launch_k(h, "bucket_init", 0, bk::bucket_init_kernel, dim3(grid_for(((u64)h->cap + 3) / 4, kMaxGrid)),
                                 dim3(kBlock), 0, h->d_parent, h->cap, (const u32*)bits, (const bk::Meta*)h->d_meta, giant);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, nvs * sizeof(u32), h->stream));
 #define GCC_P2_FINAL(PER, VW)                                                                                      \
     launch_k(h, "slice_filter", n, bk::slice_filter_kernel<true, false, PER, VW>, dim3(p2_blocks), dim3(bk::kP2Block), \
              slice_filter_lds(PER, VW), h->d_parent, (const u32*)bk_lo, (const bk::u16*)bk_hi, (const u64*)nullptr,   \
              (const u32*)bits, nw32, ns, h->d_meta, vl, cps, 65536u, slot++, h->tune.drain_at, 0u, (const u32*)giant, \
-             h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr)
+             h->d_slow, slow_cap, h->cap, h->d_err, slow2 ? h->d_seg : nullptr, bk::kVlFinal)
     rc = t.bucket_p2_per == 12 ? (t.bucket_p2_vw == 8 ? GCC_P2_FINAL(12, 8) : GCC_P2_FINAL(12, 4)) : GCC_P2_FINAL(8, 4);
 #undef GCC_P2_FINAL
     if (!rc && bucket_stats()) {  // diagnostics: FINAL P2's output (synchronises)
@@ -2563,14 +2562,14 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         HIP_TRY(hipMemcpyAsync(&hm, h->d_meta, sizeof(hm), hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(hipStreamSynchronize(h->stream));
         u64 vl_used = 0, slow = 0;
-        for (u32 s = 0; s < nvs; ++s) vl_used += std::min(hm.vl_cur[s], hm.vl_cap[s]);
+        for (u32 s = 0; s < nvs; ++s) vl_used += std::min(hm.vl_cur[bk::kVlFinal][s], hm.vl_cap[s]);
         for (u32 b = 0; b < p2_blocks; ++b) slow += hm.slow_cnt[b];
         std::fprintf(stderr, "[bucket] FINAL P2: v-list entries %llu, slow %llu (%.1f %%), slow runs %u\n",
                      (unsigned long long)vl_used, (unsigned long long)slow, 100.0 * slow / n, hm.nseg);
     }
     if (!rc)
         rc = launch_k(h, "slice_hook", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                      h->d_nbits, nw32, nvs, h->d_meta, vl, cps_v, slot++, h->cap, h->d_err);
+                      h->d_nbits, nw32, nvs, h->d_meta, vl, cps_v, slot++, h->cap, h->d_err, bk::kVlFinal);
     if (!rc)
         rc = defer ? launch_k(h, "bucket_join", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock), 0,
                               h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant, (const bk::Meta*)h->d_meta,
@@ -2586,14 +2585,14 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (slow2 && !rc) {
         // the bucket storage (consumed by FINAL P2) as u64 slow entries
         const u32 slow_cap2 = (u32)std::min<u64>(0x7FFFFFFEull, h->bk_cap_bytes / 8 / p2_blocks) & ~1u;
-        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + vl_cur_off, 0, nvs * sizeof(u32), h->stream));
         rc = launch_k(h, "slice_filter2", 0, bk::slice_filter_kernel<true, true>, dim3(p2_blocks), dim3(bk::kP2Block),
                       f_lds, h->d_parent, (const u32*)nullptr, (const bk::u16*)nullptr, (const u64*)h->d_slow,
                       (const u32*)bits, nw32, ns, h->d_meta, vl, 1u, 65536u, slot++, h->tune.drain_at, 0u,
-                      (const u32*)giant, reinterpret_cast<u64*>(h->d_bk), slow_cap2, h->cap, h->d_err, h->d_seg);
+                      (const u32*)giant, reinterpret_cast<u64*>(h->d_bk), slow_cap2, h->cap, h->d_err, h->d_seg,
+                      bk::kVlLevel2);
         if (!rc)
             rc = launch_k(h, "slice_hook2", 0, bk::slice_hook_kernel<true>, dim3(h->n_cu), dim3(bk::kP3Block), h_lds, bits,
-                          h->d_nbits, nw32, nvs, h->d_meta, vl, cps_v, slot++, h->cap, h->d_err);
+                          h->d_nbits, nw32, nvs, h->d_meta, vl, cps_v, slot++, h->cap, h->d_err, bk::kVlLevel2);
         if (!rc)
             rc = defer ? launch_k(h, "bucket_join2", 0, bk::bucket_join_kernel, dim3(grid_for(nw32, kMaxGrid)), dim3(kBlock),
                                   0, h->d_parent, bits, h->d_nbits, nw32, (const u32*)giant,
@@ -2622,7 +2621,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         u64 bk_used = 0, vl_used = 0, slow = 0;
         for (u32 s = 0; s < ns; ++s) {
             bk_used += std::min(hm.bk_cur[s], hm.bk_cap[s]);
-            vl_used += std::min(hm.vl_cur[s], hm.vl_cap[s]);
+            vl_used += std::min(hm.vl_cur[bk::kVlFinal][s], hm.vl_cap[s]);
         }
         for (u32 b = 0; b < p2_blocks; ++b) slow += hm.slow_cnt[b];
         std::fprintf(stderr, "[bucket] n=%llu ns=%u bucket entries %llu, v-list entries %llu (%.1f %%), slow %llu "
@@ -2995,7 +2994,7 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::slice_filter_kernel<true, false, 12, 8>, (int)slice_filter_lds(12, 8)},
         {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kVSliceWords * sizeof(u32))},
         {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kVSliceWords * sizeof(u32))},
-        {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
+        {(const void*)bk::bucket_layout_kernel, (int)(2 * kHubSlots * sizeof(u32))},
         {(const void*)bk::bucket_kernel<512, 16>, (int)bk::p1_lds(512, 16)},
         {(const void*)bk::bucket_kernel<1024, 16>, (int)bk::p1_lds(1024, 16)},
         {(const void*)bk::bucket_kernel<1024, 12>, (int)bk::p1_lds(1024, 12)},
@@ -3783,6 +3782,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "bucket_items") t.bucket_items = std::max(1, std::min(64, (int)value));
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
     else if (k == "bucket_defer") t.bucket_defer = value != 0.0;
+    else if (k == "bucket_defer_c") t.bucket_defer_c = value != 0.0;
     else if (k == "bucket") t.bucket = value != 0;
     else if (k == "bucket_min_batch") t.bucket_min_batch = (u64)value;
     else if (k == "bucket_min_ids") t.bucket_min_ids = (u64)value;
