@@ -71,10 +71,9 @@ struct Meta {
     u32 ring_used;               // FINAL P2 united some slow edges itself (its region was full): see bucket_join_kernel
     u32 chunk;                   // entries per chunk reservation (chunk_entries)
     u32 slow_cnt[kMaxP2Blocks];  // FINAL P2: slow edges (source not in C) each block listed in its own region
-    // the layout's sample counts, summed over its blocks; its last block reads them with atomicExch(0), so they are
-    // zero again for the next layout (zeroed once when Meta is allocated)
-    u32 lay_cu[kMaxBuckets];
-    u32 lay_cv[kMaxVLists];
+    // the layout's per-block sample counts (a row per block: source slices, then target slices; plain stores, summed
+    // by the block that arrives last) and its arrival ticket (left at zero by that block; zeroed at allocation)
+    u32 lay_rows[64][kMaxBuckets + kMaxVLists];
     u32 lay_done;
 };
 constexpr u32 kVlPasses = 8;  // Meta::vl_cur: seeding levels 0..5, FINAL (6), the second level (7)
@@ -263,12 +262,15 @@ __device__ __forceinline__ void block_prefix(const u32* cap, u64* base, u32 ns, 
     __syncthreads();
 }
 
-// Round 5: kLayoutBlocks blocks, each counting its runs of the sample in LDS and adding the counts to Meta::lay_*; the
-// block that arrives last (a ticket) computes the capacities and prefix sums (one 1024-thread block took 22 us per
-// fresh fold for the whole sample: C4 in 8 windows 0.18 ms per step). A fresh fold also clears C's bitmap here (every
-// block its share; it was a memset) and the last block elects the hub (bucket_hub_kernel until round 4): C := {h},
-// gmin := h. dynamic LDS: 2 x kHubSlots u32 when elect, else none.
+// Round 5: kLayoutBlocks blocks, one 1024-edge run of the sample each, its counts stored as a row of Meta::lay_rows
+// (plain stores behind a release; round 5's first version added them to shared counters with atomics, and 64 blocks
+// contending on the same words made the layout slower than one block: 33 against 22 us); the block that arrives last
+// (a ticket) sums the rows and computes the capacities and prefix sums. A fresh fold also clears C's bitmap here
+// (every block its share; it was a memset) and elects the hub (bucket_hub_kernel until round 4): every block runs
+// the same deterministic election, so the block that clears the hub's word sets its bit, and block 0 stores gmin.
+// dynamic LDS: 2 x kHubSlots u32 when elect, else none.
 constexpr u32 kLayoutBlocks = 64;
+static_assert(kSample / 1024 == kLayoutBlocks, "one sample run per layout block");
 __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                               Meta* __restrict__ m, u32 bk_blocks, u32 vl_blocks,
                                                               u32 chunk, u32* __restrict__ bits_clear, u32 nwords32,
@@ -279,28 +281,34 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     __shared__ u64 s_scan[1024];
     __shared__ u32 s_last;
     const u32 nvs = vslices(cap);
+    constexpr u32 kRow = kMaxBuckets + kMaxVLists;
+    u64 hs[kHubPer];
+    if (elect) hub_sample(edges, n < kHubSample ? n : kHubSample, hs);  // in flight before the run's load
+    const u64 n_smp = n < kSample ? n : kSample;
+    const u64 run_stride = n / kLayoutBlocks;  // >= 1024 whenever n >= kSample; below that the sample is the batch
+    const u32 b = blockIdx.x;                  // this block's run: 1024 CONSECUTIVE edges (coalesced)
+    const u64 k = n <= kSample ? threadIdx.x + (u64)b * 1024 : (u64)b * run_stride + threadIdx.x;
+    const u64 e = k < n ? edges[k] : ~0ull;
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
         s_cu[s] = 0;
         if (s < nvs) s_cv[s] = 0;
     }
-    if (bits_clear) {  // 16-B stores; nwords32 is even (host: 2 x 64-bit words)
+    const u32 h = elect ? hub_elect(hs, s_tab, cap) : GCC_UNSEEN_DEV;  // its barriers also order the zeroing above
+    if (!elect) __syncthreads();
+    if (bits_clear) {  // 16-B stores; nwords32 is even (host: 2 x 64-bit words). The hub's word carries its bit
         typedef u32 u4 __attribute__((ext_vector_type(4)));
-        const u4 z = {0u, 0u, 0u, 0u};
-        for (u32 w = 4 * (blockIdx.x * 1024 + threadIdx.x); w < nwords32; w += 4 * gridDim.x * 1024) {
-            if (w + 3 < nwords32) *reinterpret_cast<u4*>(bits_clear + w) = z;
-            else
-                for (u32 k = w; k < nwords32; ++k) bits_clear[k] = 0u;
+        const u32 hw = h != GCC_UNSEEN_DEV ? h >> 5 : 0xFFFFFFFFu, hb = h != GCC_UNSEEN_DEV ? 1u << (h & 31) : 0u;
+        for (u32 w = 4 * (b * 1024 + threadIdx.x); w < nwords32; w += 4 * gridDim.x * 1024) {
+            if (w + 3 < nwords32) {
+                const u4 z = {w == hw ? hb : 0u, w + 1 == hw ? hb : 0u, w + 2 == hw ? hb : 0u, w + 3 == hw ? hb : 0u};
+                *reinterpret_cast<u4*>(bits_clear + w) = z;
+            } else {
+                for (u32 x = w; x < nwords32; ++x) bits_clear[x] = x == hw ? hb : 0u;
+            }
         }
+        if (b == 0 && threadIdx.x == 0) m->gmin = h;
     }
-    __syncthreads();
-    const u64 n_smp = n < kSample ? n : kSample;
-    // the sample: kSample / 1024 = 64 runs of 1024 CONSECUTIVE edges spread evenly over the batch (coalesced, 64
-    // pages; single edges kSample apart touched 64K pages), one run per block
-    constexpr u32 kPer = kSample / 1024;
-    const u64 run_stride = n / kPer;  // >= 1024 whenever n >= kSample; below that the sample is the batch
-    for (u32 b = blockIdx.x; b < kPer; b += gridDim.x) {
-        const u64 k = n <= kSample ? threadIdx.x + (u64)b * 1024 : (u64)b * run_stride + threadIdx.x;
-        const u64 e = k < n ? edges[k] : ~0ull;
+    {
         const u32 u = (u32)e, v = (u32)(e >> 32);
         if (u < cap && v < cap) {
             atomicAdd(&s_cu[u >> kSliceBits], 1u);
@@ -309,20 +317,25 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     }
     __syncthreads();
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
-        if (s_cu[s]) atomicAdd(&m->lay_cu[s], s_cu[s]);
-        if (s < nvs && s_cv[s]) atomicAdd(&m->lay_cv[s], s_cv[s]);
+        m->lay_rows[b][s] = s_cu[s];
+        if (s < nvs) m->lay_rows[b][kMaxBuckets + s] = s_cv[s];
     }
-    __threadfence();  // release: this block's counts and bitmap zeros before its ticket
+    __threadfence();  // release: this block's row and bitmap words before its ticket
     __syncthreads();
     if (threadIdx.x == 0) s_last = atomicAdd(&m->lay_done, 1u) == gridDim.x - 1;
     __syncthreads();
     if (!s_last) return;
-    __threadfence();  // acquire: every block's counts
+    __threadfence();  // acquire: every block's row
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
-        s_cu[s] = atomicExch(&m->lay_cu[s], 0u);  // the total, and zero for the next layout
-        if (s < nvs) s_cv[s] = atomicExch(&m->lay_cv[s], 0u);
+        u32 cu = 0, cv = 0;
+        for (u32 r = 0; r < gridDim.x; ++r) {
+            cu += m->lay_rows[r][s];
+            if (s < nvs) cv += m->lay_rows[r][kMaxBuckets + s];
+        }
+        s_cu[s] = cu;
+        if (s < nvs) s_cv[s] = cv;
     }
-    if (threadIdx.x == 0) atomicExch(&m->lay_done, 0u);
+    if (threadIdx.x == 0) atomicExch(&m->lay_done, 0u);  // the next layout's ticket starts at zero
     __syncthreads();
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
         m->bk_cap[s] = est_cap(s_cu[s], n, n_smp, bk_blocks, chunk);
@@ -344,15 +357,6 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
     if (threadIdx.x == 0) {
         m->ovf_cur = 0;
         m->spill = 0;
-    }
-    if (elect) {  // the seeding's hub: the deterministic election of the seeded fold over the batch's first edges
-        u64 e[kHubPer];
-        hub_sample(edges, n < kHubSample ? n : kHubSample, e);
-        const u32 h = hub_elect(e, s_tab, cap);
-        if (threadIdx.x == 0) {
-            m->gmin = h;
-            if (h != GCC_UNSEEN_DEV) atomicOr(&bits_clear[h >> 5], 1u << (h & 31));  // after every block's zeros
-        }
     }
 }
 

@@ -1806,7 +1806,9 @@ struct FoldTune {
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
     int bucket_defer = 1;        // N labelled by the fold's closing compress instead of a store per id (bucket_join_kernel)
     // a fresh forest's C deferred like N, the reset done by P1 (round 5) instead of bucket_init_kernel's 4 B per id
-    int bucket_defer_c = 1;
+    // measured (profiles/r5c_ab_defer_c.txt, one box, interleaved): the reset's stores slow P1 by more than the launch
+    // they save (C4's share P1 0.485 -> 0.564 ms for bucket_init's 0.07), so off
+    int bucket_defer_c = 0;
     int bucket_slow2 = 1;        // second filter level over the slow edges with C | N (C4's 1/8 share: 19 % slow edges)
     int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms), 2 = 1024 x 12,
                                  // 3 = 1024 x 16 with 8-entry write-out lanes (16-B hi stores)
@@ -1825,6 +1827,7 @@ struct FoldTune {
     // the full compress's finds: read-only (0, round 5) or splitting paths in the old buffer (1, rounds 1-4; A/B only —
     // compress_bits_kernel says why not)
     int compress_split = 0;
+    int fold_split = 1;  // the plain (non-recording) fold's finds split paths (1) or are read-only (0)
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -2251,6 +2254,9 @@ static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* na
 #undef GCC_REC
     }
     h->rec_all = false;
+    if (!h->tune.fold_split)  // read-only finds in the plain fold too (A/B, round 5: the compress measured faster so)
+        return launch_k(h, name, n, fold_kernel<false, false>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent,
+                        edges, n, (u32*)nullptr, h->cap, h->d_err);
     return launch_k(h, name, n, fold_kernel<false>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent, edges, n,
                     (u32*)nullptr, h->cap, h->d_err);
 }
@@ -2450,8 +2456,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         HIP_TRY(hipMalloc((void**)&h->d_meta, sizeof(bk::Meta)));
         if (poison_scratch()) HIP_TRY(hipMemsetAsync(h->d_meta, 0xA5, sizeof(bk::Meta), h->stream));
         // the layout's sample counters start at zero (its last block leaves them zero)
-        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + offsetof(bk::Meta, lay_cu), 0,
-                               sizeof(bk::Meta) - offsetof(bk::Meta, lay_cu), h->stream));
+        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + offsetof(bk::Meta, lay_done), 0, sizeof(u32),
+                               h->stream));
     }
     const u32 p1_blocks = 2 * (u32)h->n_cu;  // (bucket_p1 = 1 runs n_cu blocks: fewer writers, same slack bound)
     const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
@@ -3773,6 +3779,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "post_check") t.post_check = std::max(0, std::min(2, (int)value));
     else if (k == "fail_absorb") t.fail_absorb = std::max(0, (int)value);
     else if (k == "compress_split") t.compress_split = value != 0;
+    else if (k == "fold_split") t.fold_split = value != 0;
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
