@@ -71,10 +71,6 @@ struct Meta {
     u32 ring_used;               // FINAL P2 united some slow edges itself (its region was full): see bucket_join_kernel
     u32 chunk;                   // entries per chunk reservation (chunk_entries)
     u32 slow_cnt[kMaxP2Blocks];  // FINAL P2: slow edges (source not in C) each block listed in its own region
-    // the layout's per-block sample counts (a row per block: source slices, then target slices; plain stores, summed
-    // by the block that arrives last) and its arrival ticket (left at zero by that block; zeroed at allocation)
-    u32 lay_rows[64][kMaxBuckets + kMaxVLists];
-    u32 lay_done;
 };
 constexpr u32 kVlPasses = 8;  // Meta::vl_cur: seeding levels 0..5, FINAL (6), the second level (7)
 constexpr u32 kVlFinal = 6, kVlLevel2 = 7;
@@ -262,80 +258,40 @@ __device__ __forceinline__ void block_prefix(const u32* cap, u64* base, u32 ns, 
     __syncthreads();
 }
 
-// Round 5: kLayoutBlocks blocks, one 1024-edge run of the sample each, its counts stored as a row of Meta::lay_rows
-// (plain stores behind a release; round 5's first version added them to shared counters with atomics, and 64 blocks
-// contending on the same words made the layout slower than one block: 33 against 22 us); the block that arrives last
-// (a ticket) sums the rows and computes the capacities and prefix sums. A fresh fold also clears C's bitmap here
-// (every block its share; it was a memset) and elects the hub (bucket_hub_kernel until round 4): every block runs
-// the same deterministic election, so the block that clears the hub's word sets its bit, and block 0 stores gmin.
-// dynamic LDS: 2 x kHubSlots u32 when elect, else none.
-constexpr u32 kLayoutBlocks = 64;
-static_assert(kSample / 1024 == kLayoutBlocks, "one sample run per layout block");
 __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                               Meta* __restrict__ m, u32 bk_blocks, u32 vl_blocks,
-                                                              u32 chunk, u32* __restrict__ bits_clear, u32 nwords32,
-                                                              u32 elect) {
+                                                              u32 chunk) {
     trace_start(kTrBkLayout);
-    extern __shared__ __attribute__((aligned(16))) u32 s_tab[];  // the hub election's table (elect only)
     __shared__ u32 s_cu[kMaxBuckets], s_cv[kMaxVLists];
     __shared__ u64 s_scan[1024];
-    __shared__ u32 s_last;
     const u32 nvs = vslices(cap);
-    constexpr u32 kRow = kMaxBuckets + kMaxVLists;
-    u64 hs[kHubPer];
-    if (elect) hub_sample(edges, n < kHubSample ? n : kHubSample, hs);  // in flight before the run's load
-    const u64 n_smp = n < kSample ? n : kSample;
-    const u64 run_stride = n / kLayoutBlocks;  // >= 1024 whenever n >= kSample; below that the sample is the batch
-    const u32 b = blockIdx.x;                  // this block's run: 1024 CONSECUTIVE edges (coalesced)
-    const u64 k = n <= kSample ? threadIdx.x + (u64)b * 1024 : (u64)b * run_stride + threadIdx.x;
-    const u64 e = k < n ? edges[k] : ~0ull;
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
         s_cu[s] = 0;
         if (s < nvs) s_cv[s] = 0;
     }
-    const u32 h = elect ? hub_elect(hs, s_tab, cap) : GCC_UNSEEN_DEV;  // its barriers also order the zeroing above
-    if (!elect) __syncthreads();
-    if (bits_clear) {  // 16-B stores; nwords32 is even (host: 2 x 64-bit words). The hub's word carries its bit
-        typedef u32 u4 __attribute__((ext_vector_type(4)));
-        const u32 hw = h != GCC_UNSEEN_DEV ? h >> 5 : 0xFFFFFFFFu, hb = h != GCC_UNSEEN_DEV ? 1u << (h & 31) : 0u;
-        for (u32 w = 4 * (b * 1024 + threadIdx.x); w < nwords32; w += 4 * gridDim.x * 1024) {
-            if (w + 3 < nwords32) {
-                const u4 z = {w == hw ? hb : 0u, w + 1 == hw ? hb : 0u, w + 2 == hw ? hb : 0u, w + 3 == hw ? hb : 0u};
-                *reinterpret_cast<u4*>(bits_clear + w) = z;
-            } else {
-                for (u32 x = w; x < nwords32; ++x) bits_clear[x] = x == hw ? hb : 0u;
+    __syncthreads();
+    const u64 n_smp = n < kSample ? n : kSample;
+    // the sample: kSample / 1024 = 64 runs of 1024 CONSECUTIVE edges spread evenly over the batch (coalesced, 64
+    // pages; single edges kSample apart touched 64K pages and took this one block 0.12 ms on C4), 32 loads in
+    // flight per thread (64 would spill)
+    constexpr u32 kPer = kSample / 1024, kBatch = 32;
+    const u64 run_stride = n / kPer;  // >= 1024 whenever n >= kSample; below that the sample is the batch
+    for (u32 b = 0; b < kPer; b += kBatch) {
+        u64 e[kBatch];
+#pragma unroll
+        for (u32 i = 0; i < kBatch; ++i) {
+            const u64 k = n <= kSample ? threadIdx.x + (u64)(b + i) * 1024 : (u64)(b + i) * run_stride + threadIdx.x;
+            e[i] = k < n ? edges[k] : ~0ull;
+        }
+#pragma unroll
+        for (u32 i = 0; i < kBatch; ++i) {
+            const u32 u = (u32)e[i], v = (u32)(e[i] >> 32);
+            if (u < cap && v < cap) {
+                atomicAdd(&s_cu[u >> kSliceBits], 1u);
+                atomicAdd(&s_cv[v >> kVSliceBits], 1u);
             }
         }
-        if (b == 0 && threadIdx.x == 0) m->gmin = h;
     }
-    {
-        const u32 u = (u32)e, v = (u32)(e >> 32);
-        if (u < cap && v < cap) {
-            atomicAdd(&s_cu[u >> kSliceBits], 1u);
-            atomicAdd(&s_cv[v >> kVSliceBits], 1u);
-        }
-    }
-    __syncthreads();
-    for (u32 s = threadIdx.x; s < ns; s += 1024) {
-        m->lay_rows[b][s] = s_cu[s];
-        if (s < nvs) m->lay_rows[b][kMaxBuckets + s] = s_cv[s];
-    }
-    __threadfence();  // release: this block's row and bitmap words before its ticket
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(&m->lay_done, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();  // acquire: every block's row
-    for (u32 s = threadIdx.x; s < ns; s += 1024) {
-        u32 cu = 0, cv = 0;
-        for (u32 r = 0; r < gridDim.x; ++r) {
-            cu += m->lay_rows[r][s];
-            if (s < nvs) cv += m->lay_rows[r][kMaxBuckets + s];
-        }
-        s_cu[s] = cu;
-        if (s < nvs) s_cv[s] = cv;
-    }
-    if (threadIdx.x == 0) atomicExch(&m->lay_done, 0u);  // the next layout's ticket starts at zero
     __syncthreads();
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
         m->bk_cap[s] = est_cap(s_cu[s], n, n_smp, bk_blocks, chunk);
@@ -344,7 +300,7 @@ __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restri
         if (s < nvs) {
             m->vl_cap[s] = est_cap(s_cv[s], n, n_smp, vl_blocks, chunk);
 #pragma unroll
-            for (u32 p = 0; p < kVlPasses; ++p) m->vl_cur[p][s] = 0;
+            for (u32 p = 0; p < kVlPasses; ++p) m->vl_cur[p][s] = 0;  // every pass's cursors (round 5: no memsets)
         }
     }
     __syncthreads();
@@ -1087,6 +1043,21 @@ __global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ p
         if (ia) hook_g(parent, g, b);
         else if (ib) hook_g(parent, g, a);
         else UF::unite(parent, a, b, c);
+    }
+}
+
+// Seeding start: clear the bitmap (done by the host's memset), elect the hub h of the batch's first edges (the
+// same deterministic election as the seeded fold), C := {h}, gmin := h. One block.
+__global__ __launch_bounds__(kHubBlock) void bucket_hub_kernel(const u64* __restrict__ edges, u64 n, u32 cap,
+                                                               u32* __restrict__ bits, Meta* __restrict__ m) {
+    trace_start(kTrBkHub);
+    extern __shared__ __attribute__((aligned(16))) u32 s_tab[];
+    u64 e[kHubPer];
+    hub_sample(edges, n < kHubSample ? n : kHubSample, e);
+    const u32 h = hub_elect(e, s_tab, cap);
+    if (threadIdx.x == 0) {
+        m->gmin = h;
+        if (h != GCC_UNSEEN_DEV) bits[h >> 5] = 1u << (h & 31);
     }
 }
 

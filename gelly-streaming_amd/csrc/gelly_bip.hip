@@ -198,6 +198,190 @@ __global__ __launch_bounds__(256) void signed_fold_giant_kernel(u32* __restrict_
     }
 }
 
+// ---- the XCD-partitioned giant fold (round 5) ----
+// The giant kernel above is bound by random 64-B line fetches of the 2-bit snapshot (16 MiB at C4's 2^26 ids: 1.7 L2
+// misses per edge, profiles/r4u_bip_pmc_*). Here the batch is first split by the SOURCE id into 8 parts of the id
+// range (one per XCD), and the blocks that serve part x all run on one XCD (blocks are dealt round-robin over the 8
+// XCDs: block b serves part b % 8 — a placement used for speed only, never for correctness), so the source's
+// snapshot lookups stay inside 1/8 of the snapshot (2 MiB at C4), which that XCD's 4 MiB L2 holds; the target's
+// stay random. The split is a one-level multi-split (kXcdParts lists, chunked reservations from a sampled layout, an
+// overflow list for a part whose estimate was low: still exact, the overflow edges take the kernel above).
+constexpr u32 kXcdParts = 8;
+constexpr int kSpBlock = 1024, kSpPer = 8;                    // split tiles of 8K edges (8 per thread, 4 x 16-B loads)
+constexpr u32 kSpTile = (u32)kSpBlock * kSpPer;
+constexpr u32 kSpChunk = 8192;                                // entries per chunk reservation
+constexpr u32 kSpSample = 1u << 16;                           // the layout's sample: 64 runs of 1024 edges
+struct XcdMeta {
+    u64 base[kXcdParts];  // part x: entries [base[x], base[x] + cap[x]) of the split buffer
+    u32 cap[kXcdParts];
+    u32 cur[kXcdParts];   // reservation cursor (may pass cap: the rest went to the overflow list)
+    u32 ovf_cur;          // overflow list cursor
+    u32 shift;            // part of a source id u: min(u >> shift, kXcdParts - 1)
+};
+__device__ __forceinline__ u32 xcd_part(u32 u, u32 shift) { const u32 x = u >> shift; return x < kXcdParts ? x : kXcdParts - 1; }
+
+// one block: capacities from a strided sample (1.25 x the estimate + one chunk per splitting block + slack, rounded
+// to 16 entries), their prefix sums; the cursors reset
+__global__ __launch_bounds__(1024) void xcd_layout_kernel(const u64* __restrict__ edges, u64 n, u32 shift, u32 blocks,
+                                                         XcdMeta* __restrict__ m) {
+    __shared__ u32 s_cnt[kXcdParts];
+    if (threadIdx.x < kXcdParts) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const u64 n_smp = n < kSpSample ? n : kSpSample, stride = n / 64;
+    for (u32 r = 0; r < 64; ++r) {
+        const u64 k = n <= kSpSample ? threadIdx.x + (u64)r * 1024 : (u64)r * stride + threadIdx.x;
+        if (k < n && threadIdx.x + (u64)r * 1024 < n_smp) atomicAdd(&s_cnt[xcd_part((u32)edges[k], shift)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u64 b = 0;
+        for (u32 x = 0; x < kXcdParts; ++x) {
+            const u64 est = (u64)s_cnt[x] * n / (n_smp ? n_smp : 1);
+            const u64 c = (est + est / 4 + 4096 + (u64)blocks * kSpChunk + 15) / 16 * 16;
+            m->base[x] = b;
+            m->cap[x] = (u32)(c < 0xFFFFFFF0ull ? c : 0xFFFFFFF0ull);
+            m->cur[x] = 0;
+            b += m->cap[x];
+        }
+        m->ovf_cur = 0;
+        m->shift = shift;
+    }
+}
+
+// the split: per tile, an LDS counting sort by part, then each part's run written contiguously into the block's
+// current chunk of that part (a new chunk from the part's cursor when it runs out); past the capacity, the overflow
+// list. The unused tail of every chunk is written ~0 at exit (the giant kernel skips it).
+__global__ __launch_bounds__(kSpBlock) void xcd_split_kernel(const u64* __restrict__ edges, u64 n, XcdMeta* __restrict__ m,
+                                                            u64* __restrict__ out, u64* __restrict__ ovf, u32 ovf_cap) {
+    __shared__ u64 s_t[kSpTile];
+    __shared__ u32 s_cnt[kXcdParts], s_start[kXcdParts], s_cpos[kXcdParts], s_cend[kXcdParts];
+    __shared__ u32 s_p1[kXcdParts], s_l1[kXcdParts], s_p2[kXcdParts], s_l2[kXcdParts];
+    typedef u32 u4 __attribute__((ext_vector_type(4)));
+    const u32 shift = m->shift;
+    if (threadIdx.x < kXcdParts) s_cpos[threadIdx.x] = s_cend[threadIdx.x] = 0;
+    const u64 ntiles = (n + kSpTile - 1) / kSpTile;
+    for (u64 t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        if (threadIdx.x < kXcdParts) s_cnt[threadIdx.x] = 0;
+        __syncthreads();  // (1) counters clear, the previous tile's write-out done
+        u64 e[kSpPer];
+        u32 rk[kSpPer];
+        const u64 t0 = t * kSpTile;
+#pragma unroll
+        for (int k = 0; k < kSpPer / 2; ++k) {  // two edges per 16-B load, coalesced
+            const u64 j = t0 + 2 * ((u64)k * kSpBlock + threadIdx.x);
+            if (j + 1 < n) {
+                const u4 q = __builtin_nontemporal_load(reinterpret_cast<const u4*>(edges + j));
+                e[2 * k] = ((u64)q.y << 32) | q.x;
+                e[2 * k + 1] = ((u64)q.w << 32) | q.z;
+            } else {
+                e[2 * k] = j < n ? edges[j] : ~0ull;
+                e[2 * k + 1] = ~0ull;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kSpPer; ++k)
+            if (e[k] != ~0ull) rk[k] = atomicAdd(&s_cnt[xcd_part((u32)e[k], shift)], 1u);
+        __syncthreads();  // (2) counts
+        if (threadIdx.x == 0) {  // part starts in the tile, and each part's run reserved (chunked)
+            u32 st = 0;
+            for (u32 x = 0; x < kXcdParts; ++x) {
+                s_start[x] = st;
+                const u32 c = s_cnt[x];
+                st += c;
+                const u32 have = s_cend[x] - s_cpos[x], a = c < have ? c : have;
+                s_p1[x] = s_cpos[x];
+                s_l1[x] = a;
+                s_cpos[x] += a;
+                s_l2[x] = 0;
+                if (c > a) {
+                    const u32 need = c - a, size = ((need > kSpChunk ? need : kSpChunk) + 15) / 16 * 16;
+                    const u32 g = atomicAdd(&m->cur[x], size), cap = m->cap[x];
+                    const u32 beg = g < cap ? g : cap, end = g >= cap ? cap : ((u64)g + size > cap ? cap : g + size);
+                    const u32 b2 = need < end - beg ? need : end - beg;
+                    s_p2[x] = beg;
+                    s_l2[x] = b2;
+                    s_cpos[x] = beg + b2;
+                    s_cend[x] = end;
+                }
+            }
+        }
+        __syncthreads();  // (3) starts and runs
+#pragma unroll
+        for (int k = 0; k < kSpPer; ++k)
+            if (e[k] != ~0ull) s_t[s_start[xcd_part((u32)e[k], shift)] + rk[k]] = e[k];
+        __syncthreads();  // (4) the tile in part order
+        const u32 tot = s_start[kXcdParts - 1] + s_cnt[kXcdParts - 1];
+        for (u32 i = threadIdx.x; i < tot; i += kSpBlock) {
+            const u64 x64 = s_t[i];
+            const u32 x = xcd_part((u32)x64, shift), r = i - s_start[x];
+            u64 pos = ~0ull;
+            if (r < s_l1[x]) pos = m->base[x] + s_p1[x] + r;
+            else if (r - s_l1[x] < s_l2[x]) pos = m->base[x] + s_p2[x] + (r - s_l1[x]);
+            if (pos != ~0ull) {
+                out[pos] = x64;
+            } else {  // the part is full (its estimate was low): the overflow list (the kernel above folds it)
+                const u32 o = atomicAdd(&m->ovf_cur, 1u);
+                if (o < ovf_cap) ovf[o] = x64;
+            }
+        }
+    }
+    __syncthreads();
+    for (u32 x = 0; x < kXcdParts; ++x)  // the unused tails of this block's chunks
+        for (u32 i = s_cpos[x] + threadIdx.x; i < s_cend[x]; i += kSpBlock) out[m->base[x] + i] = ~0ull;
+}
+
+// the giant kernel over the split batch: block b serves part b % 8 (its XCD, under round-robin placement), the
+// part's entries grid-strided over the gridDim.x / 8 blocks of that part; ~0 entries (chunk tails) skipped
+__global__ __launch_bounds__(256) void signed_fold_giant_xcd_kernel(u32* __restrict__ word, const u64* __restrict__ split,
+                                                                   const XcdMeta* __restrict__ m, u32* __restrict__ gbits,
+                                                                   const u32* __restrict__ vote, u32 min_count,
+                                                                   u32* __restrict__ fail) {
+    const u32 r = vote[0];
+    const bool none = vote[1] < min_count;  // no C (the snapshot is empty): unites without the bit lookups
+    const u32 x = blockIdx.x % kXcdParts, nb = gridDim.x / kXcdParts, bi = blockIdx.x / kXcdParts;
+    const u64 len = m->cur[x] < m->cap[x] ? m->cur[x] : m->cap[x];
+    const u64* part = split + m->base[x];
+    const u64 stride = (u64)nb * 256;
+    u32 it = 0;
+    for (u64 i = (u64)bi * 256 + threadIdx.x; i < len; i += stride, ++it) {
+        if ((it & 7) == 0 && suf::ld(fail)) return;  // a failed summary is final
+        const u64 e = __builtin_nontemporal_load(part + i);
+        if (e == ~0ull) continue;
+        const u32 u = (u32)e, v = (u32)(e >> 32);
+        if (none) {
+            sunite(word, u, v, 1u, fail);
+            continue;
+        }
+        const u32 bu = gbits[u >> 4], bv = gbits[v >> 4];
+        if (giant_edge(word, gbits, fail, r, u, v, bu >> (2 * (u & 15)), bv >> (2 * (v & 15)))) sunite(word, u, v, 1u, fail);
+    }
+}
+
+// the split's overflow list (a part whose estimate was low), and the whole batch again if even that list overflowed:
+// the giant rule per edge (exact: a check, a bit set or a unite done twice changes nothing)
+__global__ __launch_bounds__(256) void signed_fold_rest_kernel(u32* __restrict__ word, const u64* __restrict__ ovf,
+                                                              const XcdMeta* __restrict__ m, u32 ovf_cap,
+                                                              const u64* __restrict__ edges, u64 n,
+                                                              u32* __restrict__ gbits, const u32* __restrict__ vote,
+                                                              u32 min_count, u32* __restrict__ fail) {
+    const u32 r = vote[0];
+    const bool none = vote[1] < min_count;
+    const u64 stride = (u64)gridDim.x * 256;
+    const u64 no = m->ovf_cur < ovf_cap ? m->ovf_cur : ovf_cap;
+    auto one = [&](u64 e) {
+        const u32 u = (u32)e, v = (u32)(e >> 32);
+        if (none) {
+            sunite(word, u, v, 1u, fail);
+            return;
+        }
+        const u32 bu = gbits[u >> 4], bv = gbits[v >> 4];
+        if (giant_edge(word, gbits, fail, r, u, v, bu >> (2 * (u & 15)), bv >> (2 * (v & 15)))) sunite(word, u, v, 1u, fail);
+    };
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < no; i += stride) one(ovf[i]);
+    if (m->ovf_cur > ovf_cap)
+        for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) one(edges[i]);
+}
+
 // into ∪= the signed partition of `other` (any forest of the same id range, compressed or not): the triple
 // (v, parent, parity) of every seen v is the constraint sign(v) XOR sign(parent) = parity. A failed input
 // fails the result (Candidates.merge :78-81).
@@ -250,6 +434,15 @@ struct gcc_signed {
     int sample_shift = 6;    // "sample_shift": its prefix sample = batch >> shift (at least 2^20 edges)
     double min_share = 0.25; // "min_share": the voted component's share of the sampled edges, else the plain fold
     int unroll = 1;          // "unroll": edges per lane per step of the giant-filtered fold (1, 2, 4, 8)
+    // "xcd": the giant-filtered fold over the batch split by source part, one part per XCD. Measured (round 5,
+    // profiles/r5f_ab_bip_xcd.txt, interleaved on one box): C4's share mapped bipartite 7.13-7.15 ms without the split,
+    // 8.0-8.3 ms with it — the split's pass is not paid back: the target lookups and the new members' bit updates
+    // still miss, and the wave divergence around the unites stays. Off; kept as a tested knob
+    int xcd = 0;
+    u64 xcd_min = 1ull << 25; // "xcd_min": ... for batches (past the sample) of at least this many edges
+    XcdMeta* d_xm = nullptr;  // its layout
+    u64* d_split = nullptr;   // the split batch (+ the overflow list behind it)
+    u64 split_cap = 0;        // entries
     std::vector<u32> host_words;
     bool host_valid = false;
 };
@@ -271,7 +464,7 @@ static int signed_fold_plain(gcc_signed* h, const u64* edges, u64 n);
 static int signed_fold(gcc_signed* h, const u32* d_pairs, u64 n) {
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
     if (!h->giant || n < (1ull << 22) || n < h->cap / 4) return signed_fold_plain(h, edges, n);
-    const u64 s = std::min<u64>(n, std::max<u64>(1ull << 20, n >> h->sample_shift));
+    const u64 s = std::min<u64>(n, std::max<u64>(1ull << 20, n >> h->sample_shift) & ~1ull);  // even: 16-B aligned rest
     int rc = signed_fold_plain(h, edges, s);
     if (rc) return rc;
     const u64 nw = ((u64)h->cap + 15) / 16;
@@ -283,7 +476,40 @@ static int signed_fold(gcc_signed* h, const u32* d_pairs, u64 n) {
     hipLaunchKernelGGL(signed_snapshot_kernel, dim3(grid_for_n(nw, kMaxGrid)), dim3(256), 0, h->stream, h->d_word, h->cap,
                        vote, min_count, h->d_gbits);
     HIP_TRY(hipGetLastError());
-    if (n > s) {
+    if (n > s && h->xcd && n - s >= h->xcd_min && ((reinterpret_cast<uintptr_t>(edges + s) & 15) == 0)) {
+        // the split: capacities from a sample, chunked reservations, the overflow list after the parts
+        const u64 m_edges = n - s;
+        int nb = 256;
+        (void)hipDeviceGetAttribute(&nb, hipDeviceAttributeMultiprocessorCount, h->device);
+        const u64 need = m_edges + m_edges / 4 + kXcdParts * (4096 + (u64)nb * kSpChunk + 16);
+        const u32 ovf_cap = (u32)std::min<u64>(m_edges / 8 + 65536, 0xFFFFFFF0ull);
+        if (h->split_cap < need + ovf_cap) {
+            if (h->d_split) {
+                HIP_TRY(hipStreamSynchronize(h->stream));
+                HIP_TRY(hipFree(h->d_split));
+                h->d_split = nullptr;
+                h->split_cap = 0;
+            }
+            HIP_TRY(hipMalloc((void**)&h->d_split, (need + ovf_cap) * sizeof(u64)));
+            h->split_cap = need + ovf_cap;
+        }
+        if (!h->d_xm) HIP_TRY(hipMalloc((void**)&h->d_xm, sizeof(XcdMeta)));
+        u32 bits = 0;
+        while (bits < 32 && ((u64)1 << bits) < h->cap) ++bits;
+        const u32 shift = bits > 3 ? bits - 3 : 0;  // 8 parts of the id range (by the top 3 bits of an id)
+        u64* ovf = h->d_split + need;
+        hipLaunchKernelGGL(xcd_layout_kernel, dim3(1), dim3(1024), 0, h->stream, edges + s, m_edges, shift, (u32)nb, h->d_xm);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(xcd_split_kernel, dim3(nb), dim3(kSpBlock), 0, h->stream, edges + s, m_edges, h->d_xm,
+                           h->d_split, ovf, ovf_cap);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(signed_fold_giant_xcd_kernel, dim3(8 * (u32)nb), dim3(256), 0, h->stream, h->d_word, h->d_split,
+                           h->d_xm, h->d_gbits, vote, min_count, h->d_fail);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(signed_fold_rest_kernel, dim3(nb), dim3(256), 0, h->stream, h->d_word, (const u64*)ovf, h->d_xm,
+                           ovf_cap, edges + s, m_edges, h->d_gbits, vote, min_count, h->d_fail);
+        HIP_TRY(hipGetLastError());
+    } else if (n > s) {
         const dim3 g(grid_for_n(n - s, kMaxGrid));
         auto k = h->unroll >= 8 ? signed_fold_giant_kernel<8>
                  : h->unroll >= 4 ? signed_fold_giant_kernel<4>
@@ -354,6 +580,8 @@ int gcc_signed_destroy(gcc_signed* h) {
     if (h->d_spare) (void)hipFree(h->d_spare);
     if (h->d_fail) (void)hipFree(h->d_fail);
     if (h->d_gbits) (void)hipFree(h->d_gbits);
+    if (h->d_split) (void)hipFree(h->d_split);
+    if (h->d_xm) (void)hipFree(h->d_xm);
     if (h->d_stage) (void)hipFree(h->d_stage);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -447,6 +675,11 @@ int gcc_signed_tune(gcc_signed* h, const char* key, double value) {
     } else if (k == "unroll") {
         CHECK_ARG(value == 1 || value == 2 || value == 4 || value == 8, "unroll must be 1, 2, 4 or 8");
         h->unroll = (int)value;
+    } else if (k == "xcd") {
+        h->xcd = value != 0;
+    } else if (k == "xcd_min") {
+        CHECK_ARG(value >= 0, "xcd_min must be >= 0");
+        h->xcd_min = (u64)value;
     } else if (k == "min_share") {
         CHECK_ARG(value > 0 && value <= 1, "min_share must be in (0, 1]");
         h->min_share = value;

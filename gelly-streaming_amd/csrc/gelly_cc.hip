@@ -2455,9 +2455,6 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (!h->d_meta) {
         HIP_TRY(hipMalloc((void**)&h->d_meta, sizeof(bk::Meta)));
         if (poison_scratch()) HIP_TRY(hipMemsetAsync(h->d_meta, 0xA5, sizeof(bk::Meta), h->stream));
-        // the layout's sample counters start at zero (its last block leaves them zero)
-        HIP_TRY(hipMemsetAsync(reinterpret_cast<char*>(h->d_meta) + offsetof(bk::Meta, lay_done), 0, sizeof(u32),
-                               h->stream));
     }
     const u32 p1_blocks = 2 * (u32)h->n_cu;  // (bucket_p1 = 1 runs n_cu blocks: fewer writers, same slack bound)
     const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
@@ -2511,10 +2508,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const bool defer = t.bucket_defer != 0;
     const bool defer_c = fresh && defer && t.bucket_defer_c;
     u32* p1_reset = defer_c ? h->d_parent : nullptr;
-    // the layout (parallel, round 5) also clears C's bitmap and elects the hub of a fresh forest
-    rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(bk::kLayoutBlocks), dim3(1024),
-                  fresh ? 2 * kHubSlots * sizeof(u32) : 0, edges, n, ns, h->cap, h->d_meta, p1_blocks, p2_blocks, chunk,
-                  fresh ? bits : (u32*)nullptr, nw32, (u32)fresh);
+    rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta,
+                  p1_blocks, p2_blocks, chunk);
     if (!rc)
         rc = ns > 256  // beyond 2^27 ids: 512 buckets' state and the 16K-edge tile exceed the LDS; 12K-edge tiles
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 12, 512>, dim3(h->n_cu), dim3(1024),
@@ -2533,6 +2528,11 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
                  : launch_k(h, "bucket", n, bk::bucket_kernel<512, 16>, dim3(p1_blocks), dim3(512), bk::p1_lds(512, 16),
                             edges, n, ns, h->cap, h->d_meta, bk_lo, bk_hi, h->d_ovf, ovf_cap, h->d_err, p1_reset);
     if (rc) return rc;
+    if (fresh) {
+        HIP_TRY(hipMemsetAsync(bits, 0, (size_t)nw32 * sizeof(u32), h->stream));
+        rc = launch_k(h, "bucket_hub", 0, bk::bucket_hub_kernel, dim3(1), dim3(kHubBlock), 2 * kHubSlots * sizeof(u32),
+                      edges, n, h->cap, bits, h->d_meta);
+    }
     // seeding (a fresh forest): C := {hub}, then levels over the sample. A later window keeps C = the tracked
     // component's bitmap and its root (the last compress wrote both), and parent[] as it is.
     const u32 frac = (u32)std::max(0.0, std::min(65536.0, t.bucket_sample * 65536.0));
@@ -3000,7 +3000,7 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::slice_filter_kernel<true, false, 12, 8>, (int)slice_filter_lds(12, 8)},
         {(const void*)bk::slice_hook_kernel<false>, (int)(bk::kVSliceWords * sizeof(u32))},
         {(const void*)bk::slice_hook_kernel<true>, (int)(bk::kVSliceWords * sizeof(u32))},
-        {(const void*)bk::bucket_layout_kernel, (int)(2 * kHubSlots * sizeof(u32))},
+        {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
         {(const void*)bk::bucket_kernel<512, 16>, (int)bk::p1_lds(512, 16)},
         {(const void*)bk::bucket_kernel<1024, 16>, (int)bk::p1_lds(1024, 16)},
         {(const void*)bk::bucket_kernel<1024, 12>, (int)bk::p1_lds(1024, 12)},

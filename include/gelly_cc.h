@@ -201,7 +201,8 @@ int gcc_signed_device_words(gcc_signed* h, const uint32_t** d_words);
 /* speed-only knobs (results identical): "giant" (1/0: the giant-filtered fold for batches of >= 2^22 edges and
  * >= id_capacity / 4), "sample_shift" (its prefix sample = batch >> shift), "min_share" (the voted component's
  * share of sampled edges below which the batch takes the plain fold), "unroll" (1/2/4/8 edges per lane per step of
- * the giant-filtered fold). GCC_E_INVALID for an unknown key. */
+ * the giant-filtered fold), "xcd" (1/0: that fold over the batch split into 8 parts by source id, one part per XCD)
+ * and "xcd_min" (the edges past the sample from which the split is used). GCC_E_INVALID for an unknown key. */
 int gcc_signed_tune(gcc_signed* h, const char* key, double value);
 /* the emission on the device: the canonical words replace the forest (asynchronous on the forest's stream; what
  * gcc_signed_words copies out). After a failure the words are unspecified (the emitted value is (false, {})). */

@@ -164,12 +164,13 @@ def test_bench_streams_full_size(golden):
     c.close()
 
 
-@pytest.mark.parametrize("giant", [1, 0])
+@pytest.mark.parametrize("giant,xcd", [(1, 1), (1, 0), (0, 0)])
 @pytest.mark.parametrize("odd", [False, True])
-def test_kron_hubs_vs_oracle(odd, giant):
+def test_kron_hubs_vs_oracle(odd, giant, xcd):
     """A kron stream mapped bipartite (hubs: contended roots), 3 windows, every window's words vs the oracle. Window
-    1 (6M edges over 2^18 ids) takes the giant-filtered fold (gcc_signed_tune giant = 1, the default) or the plain
-    one (giant = 0); with one odd edge between two hubs' side the summary fails in that window (inside the giant:
+    1 (6M edges over 2^18 ids) takes the giant-filtered fold (gcc_signed_tune giant = 1, the default) — over the batch
+    split by source part, one part per XCD (xcd = 1, forced below its 2^25-edge default by xcd_min), or not — or the
+    plain one (giant = 0); with one odd edge between two hubs' side the summary fails in that window (inside the giant:
     the parity-bit check), and the next window's fold stops at once."""
     import torch
 
@@ -182,7 +183,7 @@ def test_kron_hubs_vs_oracle(odd, giant):
     want = orc.bip_stream(pairs, starts, V, partitions=2)
     assert want["success"][0] and (want["success"][1] != odd)  # the odd edge closes a cycle in window 1
     d = torch.from_numpy(pairs.reshape(-1).view(np.int32)).cuda()
-    c = Candidates(V).tune(giant=giant)
+    c = Candidates(V).tune(giant=giant, xcd=xcd, xcd_min=0)
     for w in range(len(starts) - 1):
         c.fold_device(d.data_ptr() + 8 * starts[w], starts[w + 1] - starts[w])
         assert c.getSuccess() == bool(want["success"][w]), w
@@ -210,7 +211,8 @@ def test_giant_fold_knobs_and_no_dominant_component():
         assert ref.getSuccess()
         ref.close()
         for knobs in ({}, {"sample_shift": 1}, {"sample_shift": 10}, {"min_share": 1.0}, {"min_share": 0.001},
-                      {"unroll": 1}, {"unroll": 8}):
+                      {"unroll": 1}, {"unroll": 8}, {"xcd": 1, "xcd_min": 0}, {"xcd": 1, "xcd_min": 0, "min_share": 1.0},
+                      {"xcd": 1, "xcd_min": 0, "sample_shift": 10}, {"xcd": 1}):
             c = Candidates(V).tune(**knobs)
             c.fold_device(d.data_ptr(), E)
             assert c.getSuccess() and np.array_equal(c.words(), want), (cfg.name, knobs)
@@ -342,3 +344,36 @@ def test_device_words_tensor_matches_host_words():
     assert t.device.type == "cuda" and t.dtype.itemsize == 4 and t.numel() == V
     assert np.array_equal(t.cpu().numpy().view(np.uint32), c.words())
     c.close()
+
+
+def test_xcd_split_overflow_and_spill():
+    """The XCD split's capacities come from a strided sample of the batch; a batch whose sampled runs (the first 1024
+    edges of every 1/64) all have their sources in part 0 while the rest of it has them in part 7 leaves part 7 a
+    capacity of its slack alone, so most of its edges overflow — and the overflow list too, so the whole batch is
+    folded again (exact: idempotent). Bipartite and with an odd edge, every word against the oracle."""
+    import torch
+
+    V = 1 << 20
+    n = 1 << 24
+    rng = np.random.default_rng(0x5EED)
+    u = rng.integers(0, 1 << 16, n, dtype=np.int64) * 2  # even ids: sources in part 0 (ids < 2^17)
+    v = rng.integers(0, V // 2, n, dtype=np.int64) * 2 + 1  # odd ids anywhere
+    s = max(1 << 20, n >> 6) & ~1                            # the signed fold's sample prefix (plain fold)
+    pos = np.arange(n) - s
+    m = n - s
+    stride = m // 64
+    far = (pos >= 0) & ((pos % stride) >= 1024)
+    u[far] = (7 << 17) + rng.integers(0, 1 << 16, int(far.sum()), dtype=np.int64) * 2  # part 7, unsampled
+    pairs = np.stack([u, v], axis=1).astype(np.uint32)
+    for odd in (False, True):
+        p = pairs.copy()
+        if odd:
+            p[n - 10] = [p[5, 0], p[7, 0]]  # two even ids
+        want = orc.bip_stream(p, [0, n], V, partitions=1)
+        d = torch.from_numpy(p.reshape(-1).view(np.int32)).cuda()
+        c = Candidates(V).tune(xcd=1, xcd_min=0, min_share=0.001)
+        c.fold_device(d.data_ptr(), n)
+        assert c.getSuccess() == bool(want["success"][0]), odd
+        if want["success"][0]:
+            assert np.array_equal(c.words(), want["words"][0])
+        c.close()
