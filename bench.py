@@ -38,6 +38,9 @@ KERNEL_BYTES = {
     "fold_kernel": (16, "edge"),            # edge + both parents
     "compress_bits_kernel": (8.125, "id"),  # parent read + label write + 1 bitmap bit
     "compress_inc_kernel": (8.125, "id"),   # the same, incremental (bloom of the window's mutations in LDS)
+    "fold_pipe_kernel": (16, "edge"),       # fold_kernel's bytes (its touched-id marks are atomics on 2 bits per id)
+    # the pipelined emission's scan: the label read + the new-id and tracked-component bits (it writes changed labels only)
+    "compress_pipe_kernel": (4.25, "id"),
     "seed_pack_kernel": (5.125, "id"),      # flag byte read + parent write + 1 bitmap bit (the init variant)
     "seed_hub_kernel": (1.125, "id"),       # flag byte + bitmap bit cleared
     # the bucketed fold's P1 runs over every edge of the batch once: priced at SURVEY §8(d)'s 16 B per edge (its own
@@ -206,7 +209,8 @@ def kernel_stats(log, V, inst_steps):
                  "bucket_slow": "bucket_slow_kernel", "bucket_rest": "bucket_rest_kernel",
                  "bucket_layout": "bucket_layout_kernel", "bucket_hub": "bucket_hub_kernel", "bucket_init": "bucket_init_kernel", "overflow": "fold_filtered_kernel",
                  "slice_filter2": "slice_filter_kernel<true,true>", "slice_hook2": "slice_hook_kernel<true> (level 2)",
-                 "bucket_hook2": "bucket_hook_kernel (level 2)"}
+                 "bucket_hook2": "bucket_hook_kernel (level 2)", "plain_pipe": "fold_pipe_kernel",
+                 "resolve": "pipe_resolve_kernel", "compress_pipe": "compress_pipe_kernel"}
     phases, kernels, spans = {}, {}, []
     for name, ms, n in log:
         if name in ("begin", "slow_edges"):

@@ -101,6 +101,7 @@ __device__ u32* gcc_trace_slot = nullptr;
 enum : u32 {
     kTrFold = 1, kTrFiltered, kTrCompressBits, kTrCompressInc, kTrSeedBfs, kTrSeedPack, kTrMergeLabels,
     kTrBkLayout, kTrBkP1, kTrBkHub, kTrBkP2Seed, kTrBkP3Seed, kTrBkInit, kTrBkP2, kTrBkP3, kTrBkHook, kTrBkSlow, kTrBkRest,
+    kTrFoldPipe, kTrResolve, kTrCompressPipe,
     kTrCount
 };
 static const char* const kTraceNames[kTrCount] = {
@@ -108,7 +109,7 @@ static const char* const kTraceNames[kTrCount] = {
     "seed_pack_kernel", "merge_labels_kernel", "bucket_layout_kernel", "bucket_kernel (P1)", "bucket_hub_kernel",
     "slice_filter_kernel<false> (P2 seed)", "slice_hook_kernel<false> (P3 seed)", "bucket_init_kernel",
     "slice_filter_kernel<true> (P2)", "slice_hook_kernel<true> (P3)", "bucket_hook_kernel", "bucket_slow_kernel",
-    "bucket_rest_kernel"};
+    "bucket_rest_kernel", "fold_pipe_kernel", "pipe_resolve_kernel", "compress_pipe_kernel"};
 __device__ __forceinline__ void trace_start(u32 id) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         u32* t = gcc_trace_slot;
@@ -853,6 +854,210 @@ __global__ __launch_bounds__(kIncBlock) void compress_inc_kernel(const u32* pare
                 else if (lab[k] != pk) gcc::st_through(labels + v0 + k, lab[k]);
             }
         chunk_bits(bits, nwords, nfull, lane, g, lab);
+    }
+}
+
+// ---- The pipelined emission (round 5; tune key inc_pipe) ----------------------------------------------------------
+// Short windows over a big forest (C5: 2^16 edges per window over 2^24 ids): the emission of window w — the
+// incremental compress, a scan of the whole label array — no longer has to finish before window w+1's fold starts.
+// The labels live in their own array L (d_spare), and the scan of window w reads only L and a snapshot taken right
+// after the fold, never parent[]: so it runs on a second stream, beside the next window's fold.
+//   fold w (fold_pipe_kernel, handle stream): the recording fold, which also marks every touched id exactly
+//     (uf_device.h PipeRec: hooked roots and new ids, 2 bits per id in `touched`);
+//   resolve w (pipe_resolve_kernel, handle stream, before fold w+1): for each touched id x, roots[x] = root(x) now,
+//     the new ids' bits copied out (`born`), `touched` cleared; the tracked root followed;
+//   scan w (compress_pipe_kernel, pipe stream, after resolve w): L[v] = roots[v] for a new v; else, when L[v]'s
+//     root l is marked in the window's bloom, L[v] = roots[l] (one load: no find); the tracked component's bitmap.
+// Why roots[l] is right: L[v] = l was a root at the end of window w-1. If l was hooked in w, roots[l] is its root at
+// the end of w. If the bloom only says "maybe" (a false positive), l was not touched in w, and roots[l] is UNSEEN or
+// was written in an earlier window of the same parity: when l was new then — and l, a root now, was one since (a
+// root is never made a root again until a reset), so roots[l] = l. The roots arrays are filled with UNSEEN when the
+// mode starts after a reset. Buffers alternate: roots and born by window parity, blooms in a ring of 3 (the scan of
+// window w clears the one fold w+2 records into); fold w+2 waits for scan w (its bloom, roots, born buffers).
+__global__ __launch_bounds__(kBlock) void fold_pipe_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
+                                                           u64 n_edges, u32* __restrict__ bloom,
+                                                           u32* __restrict__ touched, u32 cap, u32* __restrict__ err) {
+    trace_start(kTrFoldPipe);
+    NoCount c;
+    const u64 stride = (u64)gridDim.x * kBlock;
+    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n_edges; i += stride) {
+        const u64 e = __builtin_nontemporal_load(edges + i);
+        u32 a = (u32)e, b = (u32)(e >> 32);
+        if (!edge_ok(a, b, cap, err)) continue;
+        gcc::UFRec::unite(parent, a, b, c, gcc::PipeRec{bloom, touched});  // memory-side atomics only (UFRec)
+    }
+}
+
+// One thread per 32 ids (a u64 of `touched`: hooked bits | new bits << 32). The forest is quiescent here (after
+// the window's folds, before the next window's, on one stream): read-only finds. The touched words are cleared with
+// memory-side atomics (the next fold ORs into them with atomics); roots and born are written through
+// (gcc::st_through: the scan reads them from another stream, and both are rewritten two windows later).
+__global__ __launch_bounds__(kBlock) void pipe_resolve_kernel(const u32* __restrict__ parent, u64* __restrict__ touched,
+                                                              u32 nw, u32* __restrict__ roots, u32* __restrict__ born,
+                                                              const u32* __restrict__ giant_prev,
+                                                              u32* __restrict__ giant_next) {
+    trace_start(kTrResolve);
+    NoCount c;
+    u32* par = const_cast<u32*>(parent);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const u32 g0 = *giant_prev;
+        *giant_next = (g0 == UNSEEN) ? UNSEEN : UFRead::find_from(par, g0, parent[g0], c);
+    }
+    for (u32 w = blockIdx.x * kBlock + threadIdx.x; w < nw; w += gridDim.x * kBlock) {
+        const u64 t = touched[w];
+        if (!t) continue;
+        atomicExch(reinterpret_cast<unsigned long long*>(touched + w), 0ull);
+        const u32 nb = (u32)(t >> 32);
+        if (nb) gcc::st_through(born + w, nb);
+        for (u32 m = (u32)t | nb; m; m &= m - 1) {
+            const u32 x = w * 32 + (u32)__builtin_ctz(m);
+            gcc::st_through(roots + x, gcc::pipe_root(par, x));
+        }
+    }
+}
+
+// The scan of window w (one 1024-thread block per CU, the window's bloom in LDS, compress_inc_kernel's chunk layout:
+// lane l takes ids 64 j + l of each 256-id chunk, so a ballot per j is the chunk's bitmap word j). Reads L and the
+// chunk's 8 new-id words; the hits (new ids and marked labels) need a load of the roots snapshot, a load that depends
+// on the stream's: done inline, every hit would wait for the next batch's prefetch too (vmcnt is in order; the lesson
+// of compress_inc_kernel), so they are queued per wave in LDS and a flush resolves up to kIncQ at once, stores the
+// changed labels (write-through) and ORs their tracked-component bits into the words the stream already wrote.
+// Clears its new-id words and its share of `bloom_clear`.
+__global__ __launch_bounds__(kIncBlock) void compress_pipe_kernel(u32* __restrict__ labels, u32* parent, u32 n,
+                                                                  const u32* __restrict__ bloom,
+                                                                  u32* __restrict__ bloom_clear, u32* __restrict__ born,
+                                                                  const u32* __restrict__ roots,
+                                                                  const u32* __restrict__ giant, u64* __restrict__ bits) {
+    trace_start(kTrCompressPipe);
+    extern __shared__ __attribute__((aligned(16))) u32 s_bloom[];
+    __shared__ u32 s_g;
+    __shared__ u32 s_qv[kIncBlock / 64][kIncQ], s_ql[kIncBlock / 64][kIncQ];  // queued hits per wave: id, label
+    constexpr u32 kW4 = gcc::kBloomBits / 128;
+    const u32 lane = threadIdx.x & 63;
+    const u64 nwords = ((u64)n + 63) / 64;
+    const u64 nfull = (u64)n / 256;
+    const u64 nwaves = (u64)gridDim.x * (kIncBlock / 64);
+    const u64 wave = (u64)blockIdx.x * (kIncBlock / 64) + (threadIdx.x >> 6);
+    u32 pv[kIncU][4], pb[kIncU][4];
+    auto load_batch = [&](u64 base) {
+#pragma unroll
+        for (int k = 0; k < kIncU; ++k) {  // clamped, unconditional
+            const u64 ch = base + (u64)k * nwaves;
+            const u64 cc = ch < nfull ? ch : nfull - 1;
+            const u32* src = labels + cc * 256 + lane;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                pv[k][j] = src[64 * j];
+                pb[k][j] = born[cc * 8 + 2 * j + (lane >> 5)];
+            }
+        }
+    };
+    if (wave < nfull) load_batch(wave);
+    {
+        lds_fill<kIncBlock>(reinterpret_cast<u32x4*>(s_bloom), reinterpret_cast<const u32x4*>(bloom), kW4);
+        const u32 per = (kW4 + gridDim.x - 1) / gridDim.x, a = blockIdx.x * per, b = min(kW4, a + per);
+        for (u32 w = 4 * a + threadIdx.x; w < 4 * b; w += kIncBlock) atomicAnd(&bloom_clear[w], 0u);
+    }
+    if (threadIdx.x == 0) s_g = *giant;
+    __syncthreads();
+    const u32 g = s_g;
+    const bool track = g != UNSEEN;
+    const u32 wv = threadIdx.x >> 6;
+    u32 qn = 0;  // queued hits of this wave (wave-uniform)
+    auto order = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    auto settle = [&](u32 v, u32 l, u32 r) {
+        if (r != l) {
+            gcc::st_through(labels + v, r);
+            // the forest follows (a memory-side atomicMin: the next window's fold may run; r is v's root at the end
+            // of this window, the smallest id on its path now and later), so that parent[] stays as flat as the
+            // labels, as the in-place incremental compress keeps it
+            atomicMin(parent + v, r);
+        }
+        if (track && r == g)
+            __hip_atomic_fetch_or(bits + (v >> 6), 1ull << (v & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto flush = [&]() {
+        order();
+        const bool ha = lane < qn, hb = lane + 64 < qn;
+        const u32 va = ha ? s_qv[wv][lane] : 0, la = ha ? s_ql[wv][lane] : 0;
+        const u32 vb = hb ? s_qv[wv][lane + 64] : 0, lb = hb ? s_ql[wv][lane + 64] : 0;
+        const u32 qa = roots[gcc::pipe_key(va, la)], qb = roots[gcc::pipe_key(vb, lb)];  // both in flight
+        if (ha) settle(va, la, gcc::pipe_settle(la, qa));
+        if (hb) settle(vb, lb, gcc::pipe_settle(lb, qb));
+        qn = 0;
+    };
+    const u64 lt = (1ull << lane) - 1;
+    for (u64 base = wave; base < nfull; base += (u64)kIncU * nwaves) {
+        u32 cur[kIncU][4], cb[kIncU][4];
+#pragma unroll
+        for (int k = 0; k < kIncU; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cur[k][j] = pv[k][j], cb[k][j] = pb[k][j];
+        const u64 nb = base + (u64)kIncU * nwaves;
+        if (nb < nfull) load_batch(nb);  // wave-uniform
+#pragma unroll
+        for (int k = 0; k < kIncU; ++k) {
+            const u64 ch = base + (u64)k * nwaves;
+            if (ch >= nfull) break;  // wave-uniform
+            const u32 v0 = (u32)(ch * 256) + lane;
+            u32 dm = 0;
+            u64 wd[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u32 l = cur[k][j];
+                const bool d = gcc::pipe_hit(s_bloom, l, (cb[k][j] >> (lane & 31)) & 1u);
+                dm |= (u32)d << j;
+                wd[j] = __ballot(!d && track && l == g);
+                if ((lane & 31) == 0 && cb[k][j]) gcc::st_through(born + ch * 8 + 2 * j + (lane >> 5), 0u);
+            }
+            if (lane < 4) bits[ch * 4 + lane] = lane == 0 ? wd[0] : lane == 1 ? wd[1] : lane == 2 ? wd[2] : wd[3];
+            if (__ballot(dm != 0) == 0) continue;  // wave-uniform: the common chunk
+            const u32 cnt = __popc(dm);
+            const u64 b1 = __ballot(cnt & 1), b2 = __ballot(cnt & 2), b4 = __ballot(cnt & 4);
+            const u32 tot = __popcll(b1) + 2 * __popcll(b2) + 4 * __popcll(b4);
+            if (qn + tot > (u32)kIncQ) flush();
+            if (tot > (u32)kIncQ) {  // a dense chunk (more hits than the queue holds): its lookups inline
+                order();
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if ((dm >> j) & 1u) {
+                        const u32 v = v0 + 64 * j, l = cur[k][j];
+                        settle(v, l, gcc::pipe_settle(l, roots[gcc::pipe_key(v, l)]));
+                    }
+                continue;
+            }
+            u32 pos = qn + __popcll(b1 & lt) + 2 * __popcll(b2 & lt) + 4 * __popcll(b4 & lt);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((dm >> j) & 1u) {
+                    s_qv[wv][pos] = v0 + 64 * j;
+                    s_ql[wv][pos] = cur[k][j];
+                    ++pos;
+                }
+            qn += tot;
+        }
+    }
+    if (qn) flush();
+    if (nfull * 256 < n && wave == nfull % nwaves) {  // the partial last chunk: 4 consecutive ids per lane
+        const u64 v0 = nfull * 256 + 4 * lane;
+        u32 lab[4] = {UNSEEN, UNSEEN, UNSEEN, UNSEEN};
+        for (u32 k = 0; k < 4; ++k)
+            if (v0 + k < n) {
+                const u32 v = (u32)(v0 + k), l = labels[v];
+                lab[k] = gcc::pipe_label(s_bloom, roots, v, l, (born[v >> 5] >> (v & 31)) & 1u);
+                if (lab[k] != l) {
+                    gcc::st_through(labels + v, lab[k]);
+                    atomicMin(parent + v, lab[k]);
+                }
+            }
+        chunk_bits(bits, nwords, nfull, lane, g, lab);
+        // the tail's new-id words (ids nfull * 256 .. n): cleared after every lane of the wave has read them
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 8 && nfull * 8 + lane < ((u64)n + 31) / 32) gcc::st_through(born + nfull * 8 + lane, 0u);
     }
 }
 
@@ -1828,6 +2033,12 @@ struct FoldTune {
     // compress_bits_kernel says why not)
     int compress_split = 0;
     int fold_split = 1;  // the plain (non-recording) fold's finds split paths (1) or are read-only (0)
+    // the pipelined emission (round 5, compress_pipe_kernel): the incremental regime's scan of window w runs on a second
+    // stream beside window w+1's fold (2: that stream at the device's highest priority, set when it is created).
+    // Measured slower, so off (profiles/r5j_ab_inc_pipe.txt, interleaved on one box: C5 8.02 -> 12.5 ms, C3/w1M 1.59 ->
+    // 2.7 ms): the recording fold with the touched marks, the resolve and the scan sharing the CUs with the next fold
+    // cost more than the overlap returns
+    int inc_pipe = 0;
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -1891,6 +2102,21 @@ struct gcc_forest {
     bool witness_armed = false;  // the last encode already reset d_witness (stream-ordered before the next absorb)
 
     unsigned long long* d_counts = nullptr;
+
+    // the pipelined emission (compress_pipe_kernel's comment). While `pipe` is on, d_spare holds the labels of the last
+    // compressed window (L) and d_parent the live forest; fold + resolve run on `stream`, the scans on pipe_stream.
+    bool pipe = false;
+    bool pipe_dirty = false;         // folds since the last pipelined compress
+    bool pipe_roots_stale = true;    // d_proots may hold roots from before the last reset
+    u64 pipe_w = 0;                  // windows compressed since the mode started
+    hipStream_t pipe_stream = nullptr;
+    hipEvent_t pipe_ev_fold = nullptr, pipe_ev_scan[2] = {nullptr, nullptr};
+    u32* d_pbloom = nullptr;   // 3 bloom buffers (a ring)
+    u64* d_touched = nullptr;  // per 32 ids: hooked bits | new bits << 32 (zero outside a window)
+    u32* d_pborn = nullptr;    // 2 parities x nw32 words: the window's new ids (zeroed by its scan)
+    u32* d_proots = nullptr;   // 2 parities x cap: roots of the window's touched ids
+    u32 nw32() const { return (u32)(((u64)cap + 31) / 32); }
+    u32* pbloom(u64 i) const { return d_pbloom + (size_t)(i % 3) * (gcc::kBloomBits / 32); }
 
     // device-side id validation of raw device batches (edge_ok): set by a kernel, reported and cleared by the next
     // synchronising call (stream_sync_checked)
@@ -1960,7 +2186,10 @@ static void mark_mutated(gcc_forest* h, bool recorded = false) {
     h->host_valid = false;
     ++h->version;
     h->compressed = false;
-    if (!recorded) h->rec_all = false;
+    if (!recorded) {
+        h->rec_all = false;
+        h->pipe_roots_stale = true;  // conservatively: the pipelined emission's roots arrays start from UNSEEN again
+    }
 }
 
 // Every kernel of the fold pipeline goes through launch_k. Timing mode launches it with hipExtLaunchKernelGGL's
@@ -2006,10 +2235,10 @@ static int msg_launched(gcc_forest* h, const char* name) {
 }
 
 template <typename F, typename... Args>
-static int launch_k(gcc_forest* h, const char* name, u64 edges, F kernel, dim3 grid, dim3 block, size_t shmem,
-                    Args... args) {
+static int launch_ks(gcc_forest* h, hipStream_t st, const char* name, u64 edges, F kernel, dim3 grid, dim3 block,
+                     size_t shmem, Args... args) {
     if (!h->timing) {
-        hipLaunchKernelGGL(kernel, grid, block, (unsigned)shmem, h->stream, args...);
+        hipLaunchKernelGGL(kernel, grid, block, (unsigned)shmem, st, args...);
     } else {
         if (h->klog.size() > 16384) {  // nobody drains the log: keep it bounded
             h->klog.clear();
@@ -2023,16 +2252,22 @@ static int launch_k(gcc_forest* h, const char* name, u64 edges, F kernel, dim3 g
             h->kev.push_back({a, b});
         }
         const int ev = (int)h->kev_used++;
-        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shmem, h->stream, h->kev[ev].first, h->kev[ev].second, 0,
+        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shmem, st, h->kev[ev].first, h->kev[ev].second, 0,
                               args...);
         h->klog.push_back({name, ev, edges});
     }
     HIP_TRY(hipGetLastError());
     if (sync_each_launch()) {  // diagnostics: a fault is reported by the launch that caused it
-        const hipError_t e = hipStreamSynchronize(h->stream);
+        const hipError_t e = hipStreamSynchronize(st);
         if (e != hipSuccess) return set_err(GCC_E_HIP, "kernel %s: %s", name, hipGetErrorString(e));
     }
     return GCC_OK;
+}
+
+template <typename F, typename... Args>
+static int launch_k(gcc_forest* h, const char* name, u64 edges, F kernel, dim3 grid, dim3 block, size_t shmem,
+                    Args... args) {
+    return launch_ks(h, h->stream, name, edges, kernel, grid, block, shmem, args...);
 }
 
 // Synchronise the handle's stream and report an id-range error that a kernel recorded since the last check
@@ -2139,9 +2374,120 @@ static int post_check_launch(gcc_forest* h, const u32* labels, const u32* bloom)
 // whether it did (only the full compress of a filtered forest can).
 // newbits (gcc_forest_absorb_many): ids still UNSEEN that belong to the tracked component (a full compress of a
 // filtered forest; the caller checks).
+// ---- the pipelined emission's host side (compress_pipe_kernel's comment) ------------------------------------------
+// Entered by a recording fold of a compressed forest (pipe_fold); every entry point that reads the labels waits for
+// the last scan (pipe_labels_ready) and reads d_spare (labels_ptr); every other entry point leaves the mode first
+// (pipe_exit, from flush()).
+static u32* labels_ptr(const gcc_forest* h) { return h->pipe ? h->d_spare : h->d_parent; }
+
+static int pipe_labels_ready(gcc_forest* h) {  // the handle's stream waits for the last scan
+    if (h->pipe && h->pipe_w > 0) HIP_TRY(hipStreamWaitEvent(h->stream, h->pipe_ev_scan[(h->pipe_w - 1) & 1], 0));
+    return GCC_OK;
+}
+
+// Leave the mode: the handle's stream waits for the last scan. With no fold since it, L is canonical and becomes
+// d_parent (compressed, the normal bloom untouched and clear since the mode started: rec_all stays). With folds since
+// it, d_parent (the live forest) stays, its pending window's touched marks are dropped, and the next compress is full.
+static int pipe_exit(gcc_forest* h) {
+    if (!h->pipe) return GCC_OK;
+    int rc = pipe_labels_ready(h);
+    if (rc) return rc;
+    if (h->pipe_dirty) {
+        HIP_TRY(hipMemsetAsync(h->d_touched, 0, (size_t)h->nw32() * sizeof(u64), h->stream));
+        h->compressed = false;
+        h->rec_all = false;
+    } else {
+        std::swap(h->d_parent, h->d_spare);
+        h->compressed = true;
+    }
+    h->pipe = false;
+    h->pipe_dirty = false;
+    h->host_valid = false;
+    return GCC_OK;
+}
+
+static int pipe_enter(gcc_forest* h) {
+    const size_t bl = gcc::kBloomBits / 8;
+    if (!h->pipe_stream) {
+        int lo = 0, hi = 0;  // the scan first: the window's fold waits for it two windows later anyway
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&h->pipe_stream, hipStreamNonBlocking, h->tune.inc_pipe >= 2 ? hi : lo));
+        HIP_TRY(hipEventCreateWithFlags(&h->pipe_ev_fold, hipEventDisableTiming));
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&h->pipe_ev_scan[i], hipEventDisableTiming));
+        HIP_TRY(hipMalloc((void**)&h->d_pbloom, 3 * bl));
+        HIP_TRY(hipMalloc((void**)&h->d_touched, (size_t)h->nw32() * sizeof(u64)));
+        HIP_TRY(hipMalloc((void**)&h->d_pborn, 2 * (size_t)h->nw32() * sizeof(u32)));
+        HIP_TRY(hipMalloc((void**)&h->d_proots, 2 * (size_t)h->cap * sizeof(u32)));
+        HIP_TRY(hipMemsetAsync(h->d_touched, 0, (size_t)h->nw32() * sizeof(u64), h->stream));
+        HIP_TRY(hipMemsetAsync(h->d_pborn, 0, 2 * (size_t)h->nw32() * sizeof(u32), h->stream));
+        h->pipe_roots_stale = true;
+    }
+    // the labels stay where the last compress wrote them (d_parent) and become L; the forest goes on in a copy in the
+    // other buffer. Not the other way round: the other buffer held the forest two kernels ago, and a plain (path
+    // splitting) store of that fold landing late would overwrite a label (the late-store model); over the
+    // forest's copy it only writes an ancestor (tests/cpp/test_uf_replay.cpp, pipeline "pipe")
+    HIP_TRY(hipMemcpyAsync(h->d_spare, h->d_parent, (size_t)h->cap * sizeof(u32), hipMemcpyDeviceToDevice, h->stream));
+    std::swap(h->d_parent, h->d_spare);
+    if (h->pipe_roots_stale) {
+        HIP_TRY(hipMemsetAsync(h->d_proots, 0xFF, 2 * (size_t)h->cap * sizeof(u32), h->stream));
+        h->pipe_roots_stale = false;
+    }
+    HIP_TRY(hipMemsetAsync(h->d_pbloom, 0, 3 * bl, h->stream));
+    h->pipe = true;
+    h->pipe_w = 0;
+    h->pipe_dirty = false;
+    return GCC_OK;
+}
+
+// The eligibility of a recording fold for the mode: entered only from a compressed forest (d_parent = the labels)
+static bool pipe_applies(const gcc_forest* h) {
+    return h->tune.inc_pipe && !h->tune.inc_check && !h->tune.post_check && h->has_giant && h->d_bits &&
+           (h->pipe || h->compressed);
+}
+
+static int pipe_fold(gcc_forest* h, const u64* edges, u64 n, const char* name) {
+    int rc = GCC_OK;
+    if (!h->pipe) rc = pipe_enter(h);
+    if (rc) return rc;
+    // the window's first fold: scan w-2 must be done (this fold's bloom, and resolve's roots / born buffers)
+    if (!h->pipe_dirty && h->pipe_w >= 2) HIP_TRY(hipStreamWaitEvent(h->stream, h->pipe_ev_scan[h->pipe_w & 1], 0));
+    (void)name;
+    rc = launch_k(h, "plain_pipe", n, fold_pipe_kernel, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent, edges, n,
+                  h->pbloom(h->pipe_w), reinterpret_cast<u32*>(h->d_touched), h->cap, h->d_err);
+    if (rc) return rc;
+    h->pipe_dirty = true;
+    return GCC_OK;
+}
+
+static int pipe_compress(gcc_forest* h) {
+    if (!h->pipe_dirty) return GCC_OK;
+    const u64 w = h->pipe_w;
+    const int par = (int)(w & 1);
+    u32* roots = h->d_proots + (size_t)par * h->cap;
+    u32* born = h->d_pborn + (size_t)par * h->nw32();
+    const u32* gp = h->d_giant + h->giant_slot;
+    u32* gn = h->d_giant + (h->giant_slot ^ 1);
+    int rc = launch_k(h, "resolve", 0, pipe_resolve_kernel, dim3(grid_for(h->nw32(), kMaxGrid)), dim3(kBlock), 0,
+                      (const u32*)h->d_parent, h->d_touched, h->nw32(), roots, born, gp, gn);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(h->pipe_ev_fold, h->stream));
+    HIP_TRY(hipStreamWaitEvent(h->pipe_stream, h->pipe_ev_fold, 0));
+    rc = launch_ks(h, h->pipe_stream, "compress_pipe", 0, compress_pipe_kernel, dim3(h->n_cu), dim3(kIncBlock),
+                   gcc::kBloomBits / 8, h->d_spare, h->d_parent, h->cap, (const u32*)h->pbloom(w), h->pbloom(w + 2), born,
+                   (const u32*)roots, (const u32*)gn, h->d_bits);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(h->pipe_ev_scan[par], h->pipe_stream));
+    h->giant_slot ^= 1;
+    h->pipe_w = w + 1;
+    h->pipe_dirty = false;
+    h->host_valid = false;
+    return GCC_OK;
+}
+
 static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth = nullptr, bool* oth_done = nullptr,
                         const u64* newbits = nullptr) {
-    int rc = GCC_OK;
+    int rc = pipe_exit(h);
+    if (rc) return rc;
     bool inplace = false;  // the compress rewrote d_parent itself (no swap)
     const bool inc_here = inc_forest(h) && !oth && !newbits;  // masks in or out: a full compress
     if (!h->filter_enabled()) {
@@ -2220,7 +2566,8 @@ static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth =
 // splitting in the finds still shortens the forest. tune.refresh_labels = 1: a full compress instead.
 static int refresh_now(gcc_forest* h) {
     if (h->tune.refresh_labels || !h->filter_enabled()) return compress_now(h, "refresh");
-    int rc = alloc_filter(h);
+    int rc = pipe_exit(h);
+    if (!rc) rc = alloc_filter(h);
     if (rc) return rc;
     if (!h->has_giant)
         rc = launch_k(h, "vote", 0, giant_vote_kernel, dim3(1), dim3(1024), 0, h->d_parent, h->cap,
@@ -2239,6 +2586,9 @@ static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* na
     if (n == 0) return GCC_OK;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
     if (h->rec_all && n * std::max<u64>(1, h->tune.inc_div) <= (u64)h->cap) {
+        if (pipe_applies(h)) return pipe_fold(h, edges, n, name);
+        int rc = pipe_exit(h);
+        if (rc) return rc;
         const dim3 g(grid_for(n, kMaxGrid));
         u32* bl = h->bloom(h->bloom_cur);
         const int v = (h->tune.inc_split ? 0 : 1) + 2 * std::max(0, std::min(2, h->tune.fold_release));
@@ -2253,6 +2603,8 @@ static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* na
         }
 #undef GCC_REC
     }
+    int rc = pipe_exit(h);
+    if (rc) return rc;
     h->rec_all = false;
     if (!h->tune.fold_split)  // read-only finds in the plain fold too (A/B, round 5: the compress measured faster so)
         return launch_k(h, name, n, fold_kernel<false, false>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent,
@@ -2263,6 +2615,7 @@ static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* na
 
 static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (n == 0) return GCC_OK;
+    if (int rc = pipe_exit(h)) return rc;
     h->rec_all = false;  // the filtered fold does not record its mutations
     const u32 nw = h->nwords() + (h->nwords() & 1);  // u64 bitmap words, rounded to 16 B
     const bool lds = nw <= kLdsBitmapMaxWords && (double)n >= h->tune.lds_edges_per_word * (double)nw;
@@ -2317,6 +2670,7 @@ static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
 // Seeded start of a fresh forest's first batch (seed_* kernels above): hub vote, BFS passes over the
 // prefix, parent[] := C ? gmin : UNSEEN. Replaces the reset memset; leaves has_giant set, bitmap = C.
 static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
+    if (int rc = pipe_exit(h)) return rc;
     const FoldTune& t = h->tune;
     h->rec_all = false;
     int rc = alloc_filter(h);
@@ -2446,6 +2800,7 @@ static int ensure_msg_scratch(gcc_forest* h) {
 }
 
 static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
+    if (int rc = pipe_exit(h)) return rc;
     const FoldTune& t = h->tune;
     const bool fresh = h->pending_reset;  // else: a later window, C = the tracked component (bucket_applies)
     h->rec_all = false;
@@ -2821,16 +3176,31 @@ static int flush_staged(gcc_forest* h) {
     return submit_slot(h, h->staged);
 }
 
-// everything queued, and parent[] materialised: the state every non-fold entry point works on
-static int flush(gcc_forest* h) {
+// everything queued and parent[] materialised, the pipelined emission still on (folds, compresses and label reads)
+static int flush_fold(gcc_forest* h) {
     int rc = flush_staged(h);
     if (rc) return rc;
     return materialize_reset(h);
 }
 
-static int compress_async(gcc_forest* h) {
-    int rc = flush(h);
+// everything queued, parent[] materialised, and the pipelined emission left: the state every other entry point
+// works on
+static int flush(gcc_forest* h) {
+    int rc = flush_fold(h);
     if (rc) return rc;
+    return pipe_exit(h);
+}
+
+// the labels of everything folded so far, in labels_ptr(h), stream-ordered on the handle's stream — except for the
+// emission call itself in the pipelined regime (ready = false: gcc_forest_compress), whose scan the handle's stream
+// does not wait for, so that the next window's fold runs beside it; every label read waits (ready = true)
+static int compress_async(gcc_forest* h, bool ready = true) {
+    int rc = flush_fold(h);
+    if (rc) return rc;
+    if (h->pipe) {
+        rc = pipe_compress(h);
+        return rc || !ready ? rc : pipe_labels_ready(h);
+    }
     if (h->compressed) return GCC_OK;
     return compress_now(h);
 }
@@ -2840,7 +3210,7 @@ static int refresh_host(gcc_forest* h) {
     int rc = compress_async(h);
     if (rc) return rc;
     h->host_labels.resize(h->cap);
-    HIP_TRY(hipMemcpyAsync(h->host_labels.data(), h->d_parent, (size_t)h->cap * sizeof(u32), hipMemcpyDeviceToHost,
+    HIP_TRY(hipMemcpyAsync(h->host_labels.data(), labels_ptr(h), (size_t)h->cap * sizeof(u32), hipMemcpyDeviceToHost,
                            h->stream));
     rc = stream_sync_checked(h);
     if (rc) return rc;
@@ -2849,11 +3219,11 @@ static int refresh_host(gcc_forest* h) {
 }
 
 static int counts(gcc_forest* h, unsigned long long out[2]) {
-    int rc = flush(h);
+    int rc = h->pipe ? compress_async(h) : flush(h);  // a forest's seen ids and roots, or the labels' (the same counts)
     if (rc) return rc;
     if (!h->d_counts) HIP_TRY(hipMalloc((void**)&h->d_counts, 3 * sizeof(unsigned long long)));
     HIP_TRY(hipMemsetAsync(h->d_counts, 0, 2 * sizeof(unsigned long long), h->stream));
-    hipLaunchKernelGGL(count_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent, h->cap,
+    hipLaunchKernelGGL(count_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->stream, labels_ptr(h), h->cap,
                        h->d_counts);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out, h->d_counts, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
@@ -2871,7 +3241,7 @@ int gcc_forest_label_digest(gcc_forest* h, uint64_t* digest, uint64_t* n_seen, u
     if (rc) return rc;
     if (!h->d_counts) HIP_TRY(hipMalloc((void**)&h->d_counts, 3 * sizeof(unsigned long long)));
     HIP_TRY(hipMemsetAsync(h->d_counts, 0, 3 * sizeof(unsigned long long), h->stream));
-    hipLaunchKernelGGL(digest_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent, h->cap,
+    hipLaunchKernelGGL(digest_kernel, dim3(grid_for(h->cap, kMaxGrid)), dim3(kBlock), 0, h->stream, labels_ptr(h), h->cap,
                        h->d_counts);
     HIP_TRY(hipGetLastError());
     unsigned long long c[3];
@@ -2984,6 +3354,7 @@ static int set_lds_attrs_impl() {
         {(const void*)compress_inc_kernel<true, false>, (int)(gcc::kBloomBits / 8)},
         {(const void*)compress_inc_kernel<false, true>, (int)(gcc::kBloomBits / 8)},
         {(const void*)compress_inc_kernel<true, true>, (int)(gcc::kBloomBits / 8)},
+        {(const void*)compress_pipe_kernel, (int)(gcc::kBloomBits / 8)},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, false>, filtered},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true, false>, filtered},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, true>, filtered},
@@ -3081,6 +3452,17 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (!h) return GCC_OK;
     DeviceGuard g(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->pipe_stream) {
+        (void)hipStreamSynchronize(h->pipe_stream);
+        (void)hipStreamDestroy(h->pipe_stream);
+    }
+    if (h->pipe_ev_fold) (void)hipEventDestroy(h->pipe_ev_fold);
+    for (int s = 0; s < 2; ++s)
+        if (h->pipe_ev_scan[s]) (void)hipEventDestroy(h->pipe_ev_scan[s]);
+    if (h->d_pbloom) (void)hipFree(h->d_pbloom);
+    if (h->d_touched) (void)hipFree(h->d_touched);
+    if (h->d_pborn) (void)hipFree(h->d_pborn);
+    if (h->d_proots) (void)hipFree(h->d_proots);
     for (int s = 0; s < 2; ++s) {
         if (h->h_stage[s]) (void)hipHostFree(h->h_stage[s]);
         if (h->d_stage[s]) (void)hipFree(h->d_stage[s]);
@@ -3185,13 +3567,16 @@ int gcc_forest_labels_device(gcc_forest* h, const uint32_t** d_labels) {
     DeviceGuard g(h->device);
     int rc = compress_async(h);  // read-only view: the forest's caches (rec_all, compressed) stay valid
     if (rc) return rc;
-    *d_labels = h->d_parent;
+    *d_labels = labels_ptr(h);
     return GCC_OK;
 }
 
 int gcc_forest_reset(gcc_forest* h) {
     CHECK_ARG(h, "null forest");
     DeviceGuard g(h->device);
+    int rc = pipe_exit(h);
+    if (rc) return rc;
+    h->pipe_roots_stale = true;  // a root of the new forest may have been touched in the old one
     h->staged = 0;
     h->pending_reset = true;  // materialised lazily (see gcc_forest::pending_reset)
     h->rec_all = false;
@@ -3271,7 +3656,7 @@ int gcc_forest_fold_host(gcc_forest* h, const uint32_t* pairs, uint64_t n_edges)
     }
     h->host_valid = false;
     ++h->version;
-    return flush(h);
+    return flush_fold(h);
 }
 
 int gcc_forest_fold_device(gcc_forest* h, const uint32_t* d_pairs, uint64_t n_edges) {
@@ -3335,13 +3720,14 @@ int gcc_forest_fold_pinned(gcc_forest* h, const uint32_t* pairs, uint64_t n_edge
 int gcc_forest_flush(gcc_forest* h) {
     CHECK_ARG(h, "null forest");
     DeviceGuard g(h->device);
-    return flush(h);
+    return flush_fold(h);
 }
 
 int gcc_forest_sync(gcc_forest* h) {
     CHECK_ARG(h, "null forest");
     DeviceGuard g(h->device);
-    int rc = flush(h);
+    int rc = flush_fold(h);
+    if (!rc) rc = pipe_labels_ready(h);  // and the last window's scan
     if (rc) return rc;
     return stream_sync_checked(h);
 }
@@ -3668,7 +4054,7 @@ int gcc_forest_deserialize(gcc_forest* h, const void* in, uint64_t size) {
 int gcc_forest_compress(gcc_forest* h) {
     CHECK_ARG(h, "null forest");
     DeviceGuard g(h->device);
-    return compress_async(h);
+    return compress_async(h, false);
 }
 
 int gcc_forest_labels(gcc_forest* h, uint32_t* out, uint32_t n) {
@@ -3738,6 +4124,10 @@ int gcc_forest_enable_timing(gcc_forest* h, int enable) {
 
 int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     CHECK_ARG(h && key, "null argument");
+    if (h->pipe) {  // a knob may change the regime: the pipelined emission ends first
+        DeviceGuard g(h->device);
+        if (int rc = pipe_exit(h)) return rc;
+    }
     FoldTune& t = h->tune;
     const std::string k(key);
     if (k == "filter") t.filter = value != 0;
@@ -3780,6 +4170,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "fail_absorb") t.fail_absorb = std::max(0, (int)value);
     else if (k == "compress_split") t.compress_split = value != 0;
     else if (k == "fold_split") t.fold_split = value != 0;
+    else if (k == "inc_pipe") t.inc_pipe = std::max(0, std::min(2, (int)value));
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
@@ -3806,6 +4197,7 @@ int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size) {
     if (h->klog.empty()) return GCC_OK;  // nothing logged
     DeviceGuard g(h->device);
     HIP_TRY(hipStreamSynchronize(h->stream));
+    if (h->pipe_stream) HIP_TRY(hipStreamSynchronize(h->pipe_stream));
     std::string out;
     char line[160];
     // per kernel: "name ms edges"; per fold: a "begin" line first and, after its kernels, "fold_span ms edges" =
@@ -3834,11 +4226,12 @@ int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size) {
         HIP_TRY(hipEventElapsedTime(&ms, h->kev[k.ev].first, h->kev[k.ev].second));
         snprintf(line, sizeof line, "%s %.5f %llu\n", k.name, ms, (unsigned long long)k.edges);
         out += line;
-        if (in_fold && std::strcmp(k.name, "compress") != 0 && std::strcmp(k.name, "compress_inc") != 0) {  // this fold's
+        if (in_fold && std::strcmp(k.name, "compress") != 0 && std::strcmp(k.name, "compress_inc") != 0 &&
+            std::strcmp(k.name, "resolve") != 0 && std::strcmp(k.name, "compress_pipe") != 0) {  // this fold's
             if (first < 0) first = k.ev;
             last = k.ev;
             if (!std::strcmp(k.name, "filtered") || !std::strcmp(k.name, "plain") || !std::strcmp(k.name, "sample") ||
-                !std::strcmp(k.name, "bucket"))  // the bucketed fold's P1 passes over every edge of the batch once
+                !std::strcmp(k.name, "bucket") || !std::strcmp(k.name, "plain_pipe"))  // P1: every edge once
                 fold_edges += k.edges;
         } else if (in_fold) {
             close_fold();

@@ -186,12 +186,27 @@ UF_HD bool bloom_test(const u32* bloom, u32 x) {
     const u32 m = bloom_mask(x);
     return (bloom[bloom_word(x)] & m) == m;
 }
+// A fold's recording policy: mark(x) when root x is hooked (x leaves root state), born(x) when x leaves UNSEEN.
 struct NoRec {
     UF_HD void mark(u32) const {}
+    UF_HD void born(u32) const {}
 };
 struct BloomRec {
     u32* bloom;
     UF_HD void mark(u32 x) const { aor(&bloom[bloom_word(x)], bloom_mask(x)); }
+    UF_HD void born(u32) const {}
+};
+// The pipelined emission's fold (gelly_cc.hip fold_pipe_kernel, round 5): the bloom mark, and every touched id exact
+// in `touched`, two u32 words per 32 ids — [2 w] the hooked roots, [2 w + 1] the new ids — which the window's
+// resolve kernel reads (and clears) to snapshot their roots before the next window's fold runs.
+struct PipeRec {
+    u32* bloom;
+    u32* touched;
+    UF_HD void mark(u32 x) const {
+        aor(&bloom[bloom_word(x)], bloom_mask(x));
+        aor(&touched[2 * (x >> 5)], 1u << (x & 31));
+    }
+    UF_HD void born(u32 x) const { aor(&touched[2 * (x >> 5) + 1], 1u << (x & 31)); }
 };
 
 template <class L, bool SPLIT, class C = NoCount>
@@ -243,7 +258,7 @@ struct UnionFind {
         if (u == v) {  // self loop: makeSet only
             if (pu == GCC_UNSEEN_DEV) {
                 c.cas();
-                gcc::cas(&parent[u], GCC_UNSEEN_DEV, u);
+                if (gcc::cas(&parent[u], GCC_UNSEEN_DEV, u) == GCC_UNSEEN_DEV) rec.born(u);
             }
             return;
         }
@@ -270,7 +285,10 @@ struct UnionFind {
             } else if (pu < v) {  // v unseen: hang it under u's observed parent (a node of u's tree, below v)
                 c.cas();
                 const u32 o = gcc::cas(&parent[v], GCC_UNSEEN_DEV, pu);
-                if (o == GCC_UNSEEN_DEV) return;
+                if (o == GCC_UNSEEN_DEV) {
+                    rec.born(v);
+                    return;
+                }
                 pv = o;  // v became seen meanwhile
             }
         }
@@ -279,6 +297,7 @@ struct UnionFind {
             const u32 lo = u < v ? u : v, hi = u < v ? v : u;
             c.cas();
             const u32 o = gcc::cas(&parent[lo], GCC_UNSEEN_DEV, lo);
+            if (o == GCC_UNSEEN_DEV) rec.born(lo);
             u = lo;
             pu = (o == GCC_UNSEEN_DEV) ? lo : o;
             v = hi;
@@ -288,10 +307,14 @@ struct UnionFind {
             c.cas();
             if (ru < v) {
                 const u32 o = gcc::cas(&parent[v], GCC_UNSEEN_DEV, ru);
-                if (o == GCC_UNSEEN_DEV) return;  // v seen and hooked under ru in one step
+                if (o == GCC_UNSEEN_DEV) {  // v seen and hooked under ru in one step
+                    rec.born(v);
+                    return;
+                }
                 pv = o;
             } else {
                 const u32 o = gcc::cas(&parent[v], GCC_UNSEEN_DEV, v);
+                if (o == GCC_UNSEEN_DEV) rec.born(v);
                 pv = (o == GCC_UNSEEN_DEV) ? v : o;
             }
         }
@@ -309,6 +332,7 @@ struct UnionFind {
             if (old == GCC_UNSEEN_DEV) {  // unreachable for seen roots; keeps the loop finite regardless
                 old = gcc::cas(&parent[hi], GCC_UNSEEN_DEV, lo);
                 if (old == GCC_UNSEEN_DEV) {
+                    rec.born(hi);
                     rec.mark(hi);
                     return;
                 }
@@ -374,6 +398,31 @@ UF_HD u32 inc_label(const u32* parent, const u32* bloom, u32 v, u32 p) {
     if (!bloom_test(bloom, p)) return p;
     NoCount c;
     return UFRead::find_from(const_cast<u32*>(parent), v, p, c);
+}
+
+// The pipelined emission's per-id steps (gelly_cc.hip pipe_resolve_kernel / compress_pipe_kernel, round 5; shared
+// with the host replay's "pipe" pipeline). pipe_root: the root of a touched id in the quiescent forest (after the
+// window's folds, before the next window's). pipe_label: v's label after window w from its label l after window w-1,
+// whether v is new in w, the window's bloom and its roots snapshot: a new id takes its root; a label marked in the
+// bloom takes roots[l] unless that is UNSEEN (a false positive never touched since the mode started: l stays; one
+// touched two or more windows ago of the same parity was new then and has been a root since: roots[l] = l).
+// pipe_root also shortcuts the touched id to that root (a memory-side atomicMin: the root is the smallest id on the
+// path, and the forest's only writes stay atomics) — the mode writes labels elsewhere, so without it parent[] would
+// only deepen, window after window.
+UF_HD u32 pipe_root(u32* parent, u32 x) {
+    NoCount c;
+    const u32 p = ld(&parent[x]);
+    const u32 r = UFRead::find_from(parent, x, p, c);
+    if (r < p) amin(&parent[x], r);
+    return r;
+}
+// The scan's per-id test, then (batched: compress_pipe_kernel queues the hits) the roots lookup and the label. A new id
+// (no label yet: l = UNSEEN) looks up its own root; a marked label its root's.
+UF_HD bool pipe_hit(const u32* bloom, u32 l, bool born) { return born || (l != GCC_UNSEEN_DEV && bloom_test(bloom, l)); }
+UF_HD u32 pipe_key(u32 v, u32 l) { return l == GCC_UNSEEN_DEV ? v : l; }
+UF_HD u32 pipe_settle(u32 l, u32 q) { return l == GCC_UNSEEN_DEV ? q : (q == GCC_UNSEEN_DEV ? l : q); }
+UF_HD u32 pipe_label(const u32* bloom, const u32* roots, u32 v, u32 l, bool born) {
+    return pipe_hit(bloom, l, born) ? pipe_settle(l, ld(&roots[pipe_key(v, l)])) : l;
 }
 
 }  // namespace gcc

@@ -231,7 +231,12 @@ int gcc_literal_success(gcc_literal* h, int* success); /* Candidates.getSuccess 
 int gcc_literal_entries(gcc_literal* h, uint64_t* out, uint64_t cap, uint64_t* n);
 
 /* ---- summary reads (DisjointSet.find :71-85, getMatches :49-51; the emitted summary per window) ---- */
-int gcc_forest_compress(gcc_forest* h); /* async: canonical labels; afterwards gcc_forest_device_ptr = labels */
+/* async: the emission of everything folded so far (canonical labels); afterwards gcc_forest_device_ptr = labels.
+ * Short windows over a big forest (the incremental regime, tune key inc_pipe, round 5) take the PIPELINED emission:
+ * the label scan runs on the forest's second stream and the handle's stream does not wait for it, so the next window's
+ * fold overlaps it. Every label read of this API (gcc_forest_labels_device / labels / find / size / digest, sync)
+ * waits for it; a device pointer kept from before must be fetched again with gcc_forest_labels_device. */
+int gcc_forest_compress(gcc_forest* h);
 int gcc_forest_labels(gcc_forest* h, uint32_t* out, uint32_t n); /* compress + copy n labels to host */
 int gcc_forest_find(gcc_forest* h, uint32_t v, uint32_t* root); /* canonical root; GCC_UNSEEN = Java null */
 /* the raw parent array as it stands (no compress): diagnostics and tests of forest invariants */
@@ -304,7 +309,7 @@ int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, 
  * inc_min_ids, inc_div, inc_inplace, inc_check, post_check, inc_split, fold_release, experimental, refresh_labels, bucket,
  * bucket_min_batch, bucket_min_ids, bucket_levels, bucket_sample, bucket_hub_sample, bucket_p1, bucket_p2_per, bucket_p2_vw,
  * bucket_chunk, bucket_windows, bucket_items,
- * bucket_slow2, bucket_defer, bucket_defer_c, compress_split, fold_split, pin_chunk, lds_edges_per_word. Unknown keys return
+ * bucket_slow2, bucket_defer, bucket_defer_c, compress_split, fold_split, inc_pipe, pin_chunk, lds_edges_per_word. Unknown keys return
  * GCC_E_INVALID. One more key is a test hook, not a speed knob: fail_absorb = n makes the n-th next absorb fail with
  * GCC_E_INTERNAL before it launches anything (a rank's failure inside the cross-GPU group merge).
  * One setting is known to give wrong results and is refused (GCC_E_INVALID) unless `experimental` is set to 1 first:

@@ -33,6 +33,12 @@
 //                  msg_absorb_kernel (lists), then the compress
 //   init           a fresh forest's seeded / bucketed start: parent[] := C ? g : UNSEEN by plain   [product]
 //                  stores (bucket_init_kernel, seed_pack_kernel<true>), then the filtered fold, then the compress
+//   pipe           the pipelined emission (round 5): window 0 as "out", then per window the recording fold  [product]
+//                  with touched marks (fold_pipe_kernel) and, in the SAME kernel on other threads, the scan of
+//                  the previous window (compress_pipe_kernel: labels, new-id words, the bloom ring), then the
+//                  window's resolve (pipe_resolve_kernel); each emission checked after its scan
+//   pipe_allhit    pipe with every label a bloom hit (maximal false positives: the roots snapshot of untouched
+//                  labels, UNSEEN or stale by parity, decides)
 //
 // Input on stdin: V W then W window sizes, then the edges "u v". Args: pipeline mode threads seeds stale_pm [late_pm
 // [late_depth [any|plain [split|ro]]]]: late stores up to late_depth kernels late, landing over any later write or
@@ -323,9 +329,19 @@ struct Forest {
     std::vector<u32> bloom[2];
     int bloom_cur = 0;
     bool rec_all = false;
-    Forest(u32 v) : V(v), parent(v, U), spare(v, U) {
+    // the pipelined emission: labels in `spare`; roots and new-id words by window parity, blooms in a ring of 3,
+    // touched marks (hooked | new, two words per 32 ids)
+    u32 nw32;
+    std::vector<u32> roots[2], born[2], touched, pbloom[3];
+    Forest(u32 v) : V(v), parent(v, U), spare(v, U), nw32((v + 31) / 32) {
         bloom[0].assign(gcc::kBloomBits / 32, 0);
         bloom[1].assign(gcc::kBloomBits / 32, 0);
+        for (int i = 0; i < 2; ++i) {
+            roots[i].assign(v, U);
+            born[i].assign(nw32, 0);
+        }
+        touched.assign(2 * (size_t)nw32, 0);
+        for (int i = 0; i < 3; ++i) pbloom[i].assign(gcc::kBloomBits / 32, 0);
     }
 };
 
@@ -435,6 +451,64 @@ static void compress_product_inc(Forest& f, int T, u64 seed, bool through = true
     f.rec_all = true;
 }
 
+// The pipelined emission in one kernel: threads [0, T) run fold_pipe_kernel over window w's edges (bloom w % 3 and
+// the touched marks), threads [T, 2T) — when w >= 1 — compress_pipe_kernel for window w-1 (its bloom as the kernel's
+// LDS copy, its roots / new-id words of parity (w-1) % 2, clearing the bloom that window w+1 will record into): the
+// product runs them on two streams, so any interleaving of the two is possible. A scan thread takes 32-id words:
+// every id of the word labelled (gcc::pipe_label), then the word cleared.
+static void k_fold_scan(Forest& f, const Edge* e, u64 n, u32 w, int T, u64 seed, bool allhit) {
+    u32* par = f.parent.data();
+    u32* lab = f.spare.data();
+    u32* bl = f.pbloom[w % 3].data();
+    const bool scan = w >= 1;
+    const u32 sw = w - 1, p = sw & 1;
+    std::vector<u32> lds = scan ? f.pbloom[sw % 3] : std::vector<u32>();
+    if (allhit) std::fill(lds.begin(), lds.end(), ~0u);
+    u32* clear = f.pbloom[(sw + 2) % 3].data();
+    const u32 V = f.V, nw = f.nw32;
+    g_model.kernel(scan ? 2 * T : T, seed, [&](int t) {
+        if (t < T) {
+            gcc::NoCount c;
+            for (u64 i = (u64)t; i < n; i += (u64)T)
+                gcc::UFRec::unite(par, e[i].a, e[i].b, c, gcc::PipeRec{bl, f.touched.data()});
+            return;
+        }
+        const u32 s = (u32)(t - T);
+        for (u32 k = s; k < nw; k += (u32)T) {
+            const u32 bw = gcc::ld(&f.born[p][k]);
+            for (u32 b = 0; b < 32 && k * 32 + b < V; ++b) {
+                const u32 v = k * 32 + b;
+                const u32 l = gcc::ld(&lab[v]);
+                const u32 r = gcc::pipe_label(lds.data(), f.roots[p].data(), v, l, (bw >> b) & 1u);
+                if (r != l) {
+                    gcc::st_through(&lab[v], r);
+                    gcc::amin(&par[v], r);  // the forest follows the labels (concurrently with the fold's threads)
+                }
+            }
+            if (bw) gcc::st_through(&f.born[p][k], 0u);
+        }
+        for (size_t k = s; k < f.pbloom[0].size(); k += (size_t)T) __atomic_store_n(&clear[k], 0u, __ATOMIC_RELAXED);
+    });
+}
+
+// pipe_resolve_kernel for window w: per 32-id word, the touched marks taken and cleared (the product: one 64-bit
+// atomic exchange), the new ids' word written out, every touched id's root snapshot
+static void k_resolve(Forest& f, u32 w, int T, u64 seed) {
+    u32* par = f.parent.data();
+    const u32 p = w & 1, nw = f.nw32;
+    g_model.kernel(T, seed, [&](int t) {
+        for (u32 k = (u32)t; k < nw; k += (u32)T) {
+            const u32 hk = __atomic_exchange_n(&f.touched[2 * (size_t)k], 0u, __ATOMIC_RELAXED);
+            const u32 nb = __atomic_exchange_n(&f.touched[2 * (size_t)k + 1], 0u, __ATOMIC_RELAXED);
+            if (nb) gcc::st_through(&f.born[p][k], nb);
+            for (u32 m = hk | nb; m; m &= m - 1) {
+                const u32 x = k * 32 + (u32)__builtin_ctz(m);
+                gcc::st_through(&f.roots[p][x], gcc::pipe_root(par, x));
+            }
+        }
+    });
+}
+
 // fold_filtered_kernel<HOOK>'s edge handling per thread: rounds of N edges; in a round the bitmap lookups, then the
 // atomicMin hooks of (T, id > g) edges, then the PREVIOUS round's hooks settled (a hook whose old value shows that
 // the id hung elsewhere pushes (g, old) to the ring), then the round's slow edges pushed; the ring drained (up to
@@ -538,11 +612,37 @@ static int run(const std::string& pipe, u32 V, const std::vector<u64>& wstart, c
                u64 seed, std::vector<u32>& bad_windows, Failure& first) {
     Forest f(V);
     SeqUF ref(V), peer(V);
-    g_model.arrays = {{f.parent.data(), V}, {f.spare.data(), V}};
+    g_model.arrays = {{f.parent.data(), V}, {f.spare.data(), V}, {f.roots[0].data(), V}, {f.roots[1].data(), V},
+                      {f.born[0].data(), f.nw32}, {f.born[1].data(), f.nw32}};
+    std::vector<u32> want_prev;  // pipe: the previous window's labels, checked after its scan
+    int bad = 0;
+    auto check = [&](const std::vector<u32>& got, const std::vector<u32>& want, u32 win) {
+        for (u32 v = 0; v < V; ++v)
+            if (got[v] != want[v]) {
+                if (!bad++) {
+                    first.window = win;
+                    first.id = v;
+                    first.got = got[v];
+                    first.want = want[v];
+                    chain_of(f.parent, v, first.chain);
+                }
+                bad_windows.push_back(win);
+                return;
+            }
+    };
+    // forest invariant (every pipeline): a seen id points at a seen id no larger than itself
+    auto invariant = [&](u32 win) {
+        for (u32 v = 0; v < V; ++v) {
+            const u32 p = f.parent[v];
+            if (p != U && (p > v || f.parent[p] == U)) {
+                std::fprintf(stderr, "invariant broken: window %u id %u parent %u\n", win, v, p);
+                std::exit(2);
+            }
+        }
+    };
     g_model.reset_run();  // late stores of an earlier run point into its freed forest
     std::vector<char> inT(V, 0);
     u32 g = U;
-    int bad = 0;
     const u32 W = (u32)wstart.size() - 1;
     for (u32 w = 0; w < W; ++w) {
         const Edge* e = E.data() + wstart[w];
@@ -621,33 +721,39 @@ static int run(const std::string& pipe, u32 V, const std::vector<u64>& wstart, c
             if (overlap) k_absorb_bits(f, ids, R, T, ks + 3);
             k_absorb_lists(f, pairs, T, ks + 4);
             k_compress_out(f, T, ks + 5);
+        } else if (pipe == "pipe" || pipe == "pipe_allhit") {
+            if (w == 0) {  // a fresh forest: fold + full compress; then the mode starts (labels = a copy of parent[])
+                k_fold(f, e, n, T, ks + 1, false);
+                k_compress_out(f, T, ks + 2);
+                check(f.parent, ref.labels(), w);
+                // the mode starts (pipe_enter): the forest is copied (a blit: plain stores) into the other buffer and
+                // goes on there; the labels stay in the compress's buffer and become L
+                u32* src = f.parent.data();
+                u32* dst = f.spare.data();
+                g_model.kernel(T, ks + 4, [&](int t) {
+                    for (u32 v = (u32)t; v < V; v += (u32)T) gcc::st(&dst[v], src[v]);
+                });
+                std::swap(f.parent, f.spare);
+            } else {
+                k_fold_scan(f, e, n, w, T, ks + 1, pipe == "pipe_allhit");  // + the scan of window w-1
+                if (w >= 2) check(f.spare, want_prev, w - 1);
+                k_resolve(f, w, T, ks + 2);
+            }
+            want_prev = ref.labels();
+            if (w + 1 == W && w >= 1) {  // the last window's scan alone
+                k_fold_scan(f, nullptr, 0, w + 1, T, ks + 3, pipe == "pipe_allhit");
+                check(f.spare, want_prev, w);
+            }
+            invariant(w);
+            continue;
         } else {
             std::fprintf(stderr, "unknown pipeline %s\n", pipe.c_str());
             std::exit(1);
         }
         // the emission is read after the compress (the product's consumer reads after a synchronisation)
-        const std::vector<u32> want = ref.labels();
         // after the compress parent[] IS the label array (out of place: swapped in; in place: rewritten)
-        for (u32 v = 0; v < V; ++v)
-            if (f.parent[v] != want[v]) {
-                if (!bad++) {
-                    first.window = w;
-                    first.id = v;
-                    first.got = f.parent[v];
-                    first.want = want[v];
-                    chain_of(f.parent, v, first.chain);
-                }
-                bad_windows.push_back(w);
-                break;
-            }
-        // forest invariant (every pipeline): a seen id points at a seen id no larger than itself
-        for (u32 v = 0; v < V; ++v) {
-            const u32 p = f.parent[v];
-            if (p != U && (p > v || f.parent[p] == U)) {
-                std::fprintf(stderr, "invariant broken: window %u id %u parent %u\n", w, v, p);
-                std::exit(2);
-            }
-        }
+        check(f.parent, ref.labels(), w);
+        invariant(w);
     }
     return bad;
 }

@@ -556,6 +556,8 @@ KNOB_CASES = {
     "bucket_defer_c": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_defer_c": 0},
     "compress_split": {"compress_split": 1},  # round 4's full compress (splitting finds): the same labels
     "fold_split": {"fold_split": 0, "filter": 0},  # the plain fold with read-only finds
+    "inc_pipe": [{"incremental": 1, "inc_min_ids": 1024, "inc_pipe": 1},  # the pipelined emission (off by default)
+                 {"incremental": 1, "inc_min_ids": 1024, "inc_pipe": 2}],
     "bucket_hub_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_hub_sample": 0.1},
     "lds_edges_per_word": {"lds_edges_per_word": 1e9},  # the short windows take the global-bitmap filter
     "bucket_p2_per": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p2_per": 8},

@@ -8,7 +8,9 @@ splitting, none without it).
 
 Each pipeline is the kernel sequence of one product path (gelly_cc.hip): the fold + out-of-place compress, the
 bloom-recording fold + in-place incremental compress (inc_inplace), the filtered fold's atomicMin hook with its
-one-round-late settle and ring unions, and the merge absorb with its plain store of new ids. All must reproduce the
+one-round-late settle and ring unions, the merge absorb with its plain store of new ids, and (round 5) the pipelined
+emission — the scan of window w in the same kernel as window w+1's fold, on other threads, with a bloom that answers
+every label (pipe_allhit) so that the roots snapshot's UNSEEN / same-parity entries decide. All must reproduce the
 sequential labels in every window, under the controlled interleaving explorer (ASan+UBSan build) and with real
 concurrent threads (ASan and TSan builds). The in-place compress WITH path splitting (round 1's first compress) must
 FAIL: it is the named race (a thread's split store of a grandparent into slot v lands after v's owner stored v's
@@ -27,7 +29,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CPP = os.path.join(HERE, "cpp")
 ASAN = os.path.join(CPP, "build", "test_uf_replay")
 TSAN = os.path.join(CPP, "build", "test_uf_replay_tsan")
-PRODUCT = ["out", "inc", "filter", "absorb", "init"]
+PRODUCT = ["out", "inc", "filter", "absorb", "init", "pipe", "pipe_allhit"]
 
 
 @pytest.fixture(scope="module")
