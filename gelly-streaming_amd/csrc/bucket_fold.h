@@ -107,7 +107,17 @@ struct PhaseClock {
 #define GCC_PH_START(pc) (pc).start()
 #define GCC_PH_MARK(pc, k) (pc).mark(k)
 #define GCC_PH_FLUSH(pc, kern) (pc).flush(kern)
+// ... and every block's start and end on the device's constant-rate clock (wall_clock64, 100 MHz), per kernel kind:
+// 0 P1, 1 FINAL P2, 2 the second level's P2, 3 FINAL P3, 4 the second level's P3, 5 a seeding P2, 6 a seeding P3,
+// 7 the slow kernel (the last launch of a kind wins): how long each block worked against the kernel's span
+constexpr int kBtKinds = 8, kBtBlocks = 1024;
+__device__ unsigned long long gcc_blk_time[kBtKinds][kBtBlocks][2];
+#define GCC_BT(kind, which)                                                                       \
+    do {                                                                                          \
+        if (threadIdx.x == 0 && blockIdx.x < kBtBlocks) gcc_blk_time[kind][blockIdx.x][which] = wall_clock64(); \
+    } while (0)
 #else
+#define GCC_BT(kind, which) (void)0
 struct PhaseClock {};
 #define GCC_PH_START(pc) (void)0
 #define GCC_PH_MARK(pc, k) (void)0
@@ -369,6 +379,7 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
                                                           u16* __restrict__ bk_hi, u64* __restrict__ ovf, u32 ovf_cap,
                                                           u32* __restrict__ err, u32* __restrict__ reset) {
     trace_start(kTrBkP1);
+    GCC_BT(0, 0);
     // the tile in bucket order: dynamic LDS (p1_lds: P1B * P1P + 3 MAXB u64, 66 / 130 KiB), set up like every
     // kernel's LDS beyond 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-bucket state below is static (MAXB >= ns)
     static_assert(MAXB <= kMaxBuckets, "Meta holds kMaxBuckets buckets");
@@ -512,6 +523,7 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
     // the unused tails of this block's chunks: padding entries (P2 skips them)
     for (u32 s = 0; s < ns; ++s)
         for (u32 i = s_cpos[s] + threadIdx.x; i < s_cend[s]; i += P1B) bk_hi[s_base[s] + i] = kPadHi;
+    GCC_BT(0, 1);
 }
 
 // Work items of P2 / P3: item i -> (slice i / cps, part i % cps) of a list of `len` entries; the part's range.
@@ -568,6 +580,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
                                                                 SlowSeg* __restrict__ segs, u32 pass) {
     static_assert(FINAL || !SEG, "the second level is a FINAL pass");
     trace_start(FINAL ? kTrBkP2 : kTrBkP2Seed);
+    GCC_BT(FINAL ? (SEG ? 2 : 1) : 5, 0);
     extern __shared__ __attribute__((aligned(16))) u32 s_dyn[];
     u32* s_bits = s_dyn;                                   // kSliceWords
     u32* s_vt = s_dyn + kSliceWords;                       // p2_tile(PER, VW): the round's targets + run padding
@@ -852,6 +865,7 @@ __global__ __launch_bounds__(kP2Block) void slice_filter_kernel(u32* __restrict_
         }
         if (threadIdx.x == 0) m->slow_cnt[blockIdx.x] = s_slow < slow_cap ? s_slow : slow_cap;
     }
+    GCC_BT(FINAL ? (SEG ? 2 : 1) : 5, 1);
 }
 
 // ---- P3: the target slice ------------------------------------------------------------------------------------
@@ -870,6 +884,7 @@ __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ 
                                                               VList vl, u32 cps, u32 work_slot,
                                                               u32 cap, u32* __restrict__ err, u32 pass) {
     trace_start(FINAL ? kTrBkP3 : kTrBkP3Seed);
+    GCC_BT(FINAL ? (pass == kVlLevel2 ? 4 : 3) : 6, 0);
     extern __shared__ __attribute__((aligned(16))) u32 s_bits[];  // kVSliceWords
     __shared__ u32 s_item, s_min;
     u32 cur_slice = 0xFFFFFFFFu;
@@ -945,6 +960,7 @@ __global__ __launch_bounds__(kP3Block) void slice_hook_kernel(u32* __restrict__ 
         __syncthreads();
         if (threadIdx.x == 0 && s_min != 0xFFFFFFFFu) atomicMin(&m->gmin, s_min);
     }
+    GCC_BT(FINAL ? (pass == kVlLevel2 ? 4 : 3) : 6, 1);
 }
 
 // N (ids reached from C by the FINAL pass) joins g's tree, each id once: a new id above g by a plain store (in this
@@ -1024,10 +1040,14 @@ __global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ p
                                                              const u32* __restrict__ bits, const u32* __restrict__ giant,
                                                              u32 cap, u32* __restrict__ err) {
     trace_start(kTrBkSlow);
+    GCC_BT(7, 0);
     const u32 g = *giant;
     NoCount c;
     const u32 r = blockIdx.x / kSlowSplit, part = blockIdx.x % kSlowSplit;
-    if (r >= nblocks) return;
+    if (r >= nblocks) {
+        GCC_BT(7, 1);
+        return;
+    }
     const u32 cnt = m->slow_cnt[r];
     const u64* list = slow + (u64)r * slow_cap;
     for (u32 k = part * kBlock + threadIdx.x; k < cnt; k += kSlowSplit * kBlock) {
@@ -1044,6 +1064,7 @@ __global__ __launch_bounds__(kBlock) void bucket_slow_kernel(u32* __restrict__ p
         else if (ib) hook_g(parent, g, a);
         else UF::unite(parent, a, b, c);
     }
+    GCC_BT(7, 1);
 }
 
 // Seeding start: clear the bitmap (done by the host's memset), elect the hub h of the batch's first edges (the

@@ -3026,6 +3026,33 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
             }
         unsigned long long zero[2][16] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(bk::gcc_phase_acc), zero, sizeof(zero)));
+        // every block's working time against the kernel's span (load balance of the persistent / work-queue kernels)
+        std::vector<unsigned long long> bt((size_t)bk::kBtKinds * bk::kBtBlocks * 2);
+        HIP_TRY(hipMemcpyFromSymbol(bt.data(), HIP_SYMBOL(bk::gcc_blk_time), bt.size() * sizeof(unsigned long long)));
+        static const char* const bt_names[bk::kBtKinds] = {"P1", "FINAL P2", "level-2 P2", "FINAL P3", "level-2 P3",
+                                                        "seed P2", "seed P3", "slow"};
+        for (int k = 0; k < bk::kBtKinds; ++k) {
+            unsigned long long lo = ~0ull, hi = 0, busy = 0, mx = 0;
+            u32 nb = 0;
+            std::vector<unsigned long long> d;
+            for (int b = 0; b < bk::kBtBlocks; ++b) {
+                const unsigned long long t0 = bt[((size_t)k * bk::kBtBlocks + b) * 2], t1 = bt[((size_t)k * bk::kBtBlocks + b) * 2 + 1];
+                if (!t0 || t1 < t0) continue;
+                lo = std::min(lo, t0);
+                hi = std::max(hi, t1);
+                busy += t1 - t0;
+                mx = std::max(mx, t1 - t0);
+                d.push_back(t1 - t0);
+                ++nb;
+            }
+            if (!nb) continue;
+            std::sort(d.begin(), d.end());
+            std::fprintf(stderr, "[blocks] %s: %u blocks, span %.1f us, block time median %.1f / max %.1f us, "
+                         "utilisation %.2f\n", bt_names[k], nb, (hi - lo) / 100.0, d[d.size() / 2] / 100.0, mx / 100.0,
+                         (double)busy / ((double)nb * (double)(hi - lo ? hi - lo : 1)));
+        }
+        std::fill(bt.begin(), bt.end(), 0ull);
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(bk::gcc_blk_time), bt.data(), bt.size() * sizeof(unsigned long long)));
 #endif
     }
     return GCC_OK;
