@@ -2007,12 +2007,18 @@ struct FoldTune {
     // 0.25 / 0.3: 10.04 / 10.06 / 10.22 / 10.33 ms, profiles/r3h_sweep_seed_sample.log)
     int bucket_levels = 2;
     double bucket_sample = 0.15;
+    // ... and for a SPARSE batch (fewer than 4 edges per id of the range: C4's 1/8 share has 2), where 36.5 % of the
+    // edges still had a source outside C after seeding at 0.15 and went through the second level: 0.3 (round 5, one box,
+    // interleaved: the share 1.875 -> 1.851 ms; 0.5: 1.936; a third level at 0.15: 1.849-1.853; profiles/r5n_*)
+    double bucket_sample_sparse = 0.3;
     double bucket_hub_sample = 1.0;  // the first level's share of the hub's bucket (C = {h}: one slice)
     u64 pin_chunk = 1ull << 25;  // gcc_forest_fold_pinned: edges per H2D chunk (256 MiB)
     int bucket_defer = 1;        // N labelled by the fold's closing compress instead of a store per id (bucket_join_kernel)
     // a fresh forest's C deferred like N, the reset done by P1 (round 5) instead of bucket_init_kernel's 4 B per id
     // measured (profiles/r5c_ab_defer_c.txt, one box, interleaved): the reset's stores slow P1 by more than the launch
     // they save (C4's share P1 0.485 -> 0.564 ms for bucket_init's 0.07), so off
+    // 2 (round 5): C deferred the same way, the reset a memset of parent[] on a second stream beside P1 and the seeding
+    // (neither touches parent[]), joined before the first kernel that does
     int bucket_defer_c = 0;
     int bucket_slow2 = 1;        // second filter level over the slow edges with C | N (C4's 1/8 share: 19 % slow edges)
     int bucket_p1 = 1;           // P1 geometry (bucket_fold.h): 0 = 512 x 16, 1 = 1024 x 16 (C4: 4.43 -> 4.25 ms), 2 = 1024 x 12,
@@ -2126,6 +2132,8 @@ struct gcc_forest {
     // gcc_forest_fold_pinned: chunks of a pinned host batch go H2D on copy_stream into two device slots while
     // the previous chunk folds on `stream`
     hipStream_t copy_stream = nullptr;
+    hipStream_t aux_stream = nullptr;  // tune bucket_defer_c = 2: the fresh forest's reset beside P1
+    hipEvent_t aux_ev[2] = {nullptr, nullptr};
     u32* d_pin[2] = {nullptr, nullptr};
     u64 pin_cap = 0;  // edges per slot
     hipEvent_t pin_copied[2] = {nullptr, nullptr}, pin_folded[2] = {nullptr, nullptr};
@@ -2845,7 +2853,8 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     // small batch) takes fewer, longer parts, about 64K edges per part at least
     const bool slow2 = t.bucket_slow2 != 0;
     if (slow2 && (rc = grow(h->d_seg, h->seg_cap, (u64)ns * cps + 64, h->stream))) return rc;
-    const u32 cps_seed = (u32)std::max<u64>(1, std::min<u64>(cps, (u64)((double)n * t.bucket_sample) / ((u64)ns << 16)));
+    const double sample = n < 4 * (u64)h->cap ? t.bucket_sample_sparse : t.bucket_sample;
+    const u32 cps_seed = (u32)std::max<u64>(1, std::min<u64>(cps, (u64)((double)n * sample) / ((u64)ns << 16)));
     // the first level streams only the hub's slice: one slice's sample, about 16K edges per part (one part per
     // P2 block at most)
     const u32 cps_hub = (u32)std::max<u64>(1, std::min<u64>(p2_blocks, (u64)((double)n * t.bucket_hub_sample) / ns / 16384));
@@ -2862,7 +2871,18 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     // a fresh forest with the deferred N: C is deferred too (round 5), and P1 performs the lazy reset itself
     const bool defer = t.bucket_defer != 0;
     const bool defer_c = fresh && defer && t.bucket_defer_c;
-    u32* p1_reset = defer_c ? h->d_parent : nullptr;
+    u32* p1_reset = defer_c && t.bucket_defer_c == 1 ? h->d_parent : nullptr;
+    if (defer_c && t.bucket_defer_c == 2) {  // the reset beside P1, ordered after everything queued before this fold
+        if (!h->aux_stream) {
+            HIP_TRY(hipStreamCreateWithFlags(&h->aux_stream, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&h->aux_ev[0], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&h->aux_ev[1], hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(h->aux_ev[0], h->stream));
+        HIP_TRY(hipStreamWaitEvent(h->aux_stream, h->aux_ev[0], 0));
+        HIP_TRY(hipMemsetAsync(h->d_parent, 0xFF, (size_t)h->cap * sizeof(u32), h->aux_stream));
+        HIP_TRY(hipEventRecord(h->aux_ev[1], h->aux_stream));
+    }
     rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta,
                   p1_blocks, p2_blocks, chunk);
     if (!rc)
@@ -2890,7 +2910,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     }
     // seeding (a fresh forest): C := {hub}, then levels over the sample. A later window keeps C = the tracked
     // component's bitmap and its root (the last compress wrote both), and parent[] as it is.
-    const u32 frac = (u32)std::max(0.0, std::min(65536.0, t.bucket_sample * 65536.0));
+    const u32 frac = (u32)std::max(0.0, std::min(65536.0, sample * 65536.0));
     const u64 sample_edges = (u64)((double)n * frac / 65536.0);
     const int levels = fresh ? std::max(0, std::min(6, t.bucket_levels)) : 0;
     for (int l = 0; l < levels && !rc; ++l) {
@@ -2905,6 +2925,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     }
     // parent[] := C ? g : UNSEEN (the reset), then every bucketed edge, the overflow list, a spill. With C deferred,
     // P1 did the reset and only g is published here
+    if (!rc && defer_c && t.bucket_defer_c == 2) HIP_TRY(hipStreamWaitEvent(h->stream, h->aux_ev[1], 0));  // the reset
     if (!rc && fresh)
         rc = defer_c ? launch_k(h, "bucket_init", 0, bk::bucket_root_kernel, dim3(1), dim3(1), 0,
                                 (const bk::Meta*)h->d_meta, giant)
@@ -3484,6 +3505,12 @@ int gcc_forest_destroy(gcc_forest* h) {
         (void)hipStreamDestroy(h->pipe_stream);
     }
     if (h->pipe_ev_fold) (void)hipEventDestroy(h->pipe_ev_fold);
+    if (h->aux_stream) {
+        (void)hipStreamSynchronize(h->aux_stream);
+        (void)hipStreamDestroy(h->aux_stream);
+    }
+    for (int s = 0; s < 2; ++s)
+        if (h->aux_ev[s]) (void)hipEventDestroy(h->aux_ev[s]);
     for (int s = 0; s < 2; ++s)
         if (h->pipe_ev_scan[s]) (void)hipEventDestroy(h->pipe_ev_scan[s]);
     if (h->d_pbloom) (void)hipFree(h->d_pbloom);
@@ -4207,12 +4234,13 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "bucket_items") t.bucket_items = std::max(1, std::min(64, (int)value));
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
     else if (k == "bucket_defer") t.bucket_defer = value != 0.0;
-    else if (k == "bucket_defer_c") t.bucket_defer_c = value != 0.0;
+    else if (k == "bucket_defer_c") t.bucket_defer_c = std::max(0, std::min(2, (int)value));
     else if (k == "bucket") t.bucket = value != 0;
     else if (k == "bucket_min_batch") t.bucket_min_batch = (u64)value;
     else if (k == "bucket_min_ids") t.bucket_min_ids = (u64)value;
     else if (k == "bucket_levels") t.bucket_levels = std::max(0, std::min(6, (int)value));
     else if (k == "bucket_sample") t.bucket_sample = std::max(0.0, std::min(1.0, value));
+    else if (k == "bucket_sample_sparse") t.bucket_sample_sparse = std::max(0.0, std::min(1.0, value));
     else if (k == "bucket_hub_sample") t.bucket_hub_sample = std::max(0.0, std::min(1.0, value));
     else return set_err(GCC_E_INVALID, "unknown tuning key '%s'", key);
     return GCC_OK;

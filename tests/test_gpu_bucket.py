@@ -56,7 +56,8 @@ def mismatch(got, want):
                                    {"bucket_sample": 0.0}, {"bucket_levels": 6, "bucket_sample": 0.05},
                                    {"bucket_slow2": 0}, {"bucket_levels": 0, "bucket_slow2": 0},
                                    {"bucket_hub_sample": 0.0}, {"bucket_levels": 3, "bucket_hub_sample": 0.15},
-                                   {"bucket_defer": 0}, {"bucket_defer": 0, "bucket_slow2": 0}])
+                                   {"bucket_defer": 0}, {"bucket_defer": 0, "bucket_slow2": 0},
+                                   {"bucket_defer_c": 1}, {"bucket_defer_c": 2}, {"bucket_defer_c": 2, "bucket_slow2": 0}])
 def test_bucketed_fold_rmat(torch_cuda, knobs):
     """R-MAT s20, 2^22 edges, one fresh batch through the bucketed fold (seeding knobs vary the sample and the
     level count: the result may not depend on them)."""
@@ -76,6 +77,22 @@ def test_bucketed_fold_rmat(torch_cuda, knobs):
         # later batches of the same forest take the filtered path against the bucketed fold's bitmap
         ds.fold_device(d.data_ptr(), E // 3)
         assert mismatch(ds.labels(), want) is None
+
+
+@pytest.mark.parametrize("knobs", [{}, {"bucket_sample_sparse": 0.0}, {"bucket_sample_sparse": 1.0},
+                                   {"bucket_defer_c": 2}])
+def test_bucketed_fold_sparse_batch(torch_cuda, knobs):
+    """A sparse batch (2 edges per id, like C4's 1/8 share): its seeding samples bucket_sample_sparse of every bucket
+    (round 5); many edges reach the second level. The result may not depend on the sample."""
+    cfg = G.scaled(G.CONFIGS["c2_rmat20"], n_edges=1 << 21, seed=0x5A5A)
+    E, V = cfg.info()
+    pairs = G.generate_host(cfg)
+    want = oracle_labels(pairs, V)
+    d = to_device(torch_cuda, pairs)
+    with DisjointSet(V) as ds:
+        ds.tune(**FORCE, **knobs)
+        ds.fold_device(d.data_ptr(), E)
+        assert mismatch(ds.labels(), want) is None, mismatch(ds.labels(), want)
 
 
 def test_bucketed_fold_gnm_no_giant(torch_cuda):

@@ -548,12 +548,14 @@ KNOB_CASES = {
     "bucket_min_ids": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16},
     "bucket_levels": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_levels": 1},
     "bucket_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_sample": 1.0},
+    "bucket_sample_sparse": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_sample_sparse": 0.05},
     "pin_chunk": {"pin_chunk": 4096},
     "bucket_p1": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 0},
                   {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 3}],
     "bucket_slow2": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_slow2": 0},
     "bucket_defer": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_defer": 0},
-    "bucket_defer_c": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_defer_c": 0},
+    "bucket_defer_c": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_defer_c": 1},
+                       {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_defer_c": 2}],
     "compress_split": {"compress_split": 1},  # round 4's full compress (splitting finds): the same labels
     "fold_split": {"fold_split": 0, "filter": 0},  # the plain fold with read-only finds
     "inc_pipe": [{"incremental": 1, "inc_min_ids": 1024, "inc_pipe": 1},  # the pipelined emission (off by default)
