@@ -2453,13 +2453,12 @@ static bool pipe_applies(const gcc_forest* h) {
            (h->pipe || h->compressed);
 }
 
-static int pipe_fold(gcc_forest* h, const u64* edges, u64 n, const char* name) {
+static int pipe_fold(gcc_forest* h, const u64* edges, u64 n) {
     int rc = GCC_OK;
     if (!h->pipe) rc = pipe_enter(h);
     if (rc) return rc;
     // the window's first fold: scan w-2 must be done (this fold's bloom, and resolve's roots / born buffers)
     if (!h->pipe_dirty && h->pipe_w >= 2) HIP_TRY(hipStreamWaitEvent(h->stream, h->pipe_ev_scan[h->pipe_w & 1], 0));
-    (void)name;
     rc = launch_k(h, "plain_pipe", n, fold_pipe_kernel, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent, edges, n,
                   h->pbloom(h->pipe_w), reinterpret_cast<u32*>(h->d_touched), h->cap, h->d_err);
     if (rc) return rc;
@@ -2594,7 +2593,7 @@ static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* na
     if (n == 0) return GCC_OK;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
     if (h->rec_all && n * std::max<u64>(1, h->tune.inc_div) <= (u64)h->cap) {
-        if (pipe_applies(h)) return pipe_fold(h, edges, n, name);
+        if (pipe_applies(h)) return pipe_fold(h, edges, n);
         int rc = pipe_exit(h);
         if (rc) return rc;
         const dim3 g(grid_for(n, kMaxGrid));
