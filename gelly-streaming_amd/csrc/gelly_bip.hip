@@ -24,12 +24,15 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "abi_common.h"
 #include "gelly_cc.h"
+#include "signed_bucket_api.h"  // the bucketed fold (gelly_cc.hip, signed_bucket.h)
 #include "signed_uf.h"  // find / seen / unite, shared with the host replay (tests/cpp/test_signed_uf.cpp)
 
 namespace {
@@ -443,6 +446,17 @@ struct gcc_signed {
     XcdMeta* d_xm = nullptr;  // its layout
     u64* d_split = nullptr;   // the split batch (+ the overflow list behind it)
     u64 split_cap = 0;        // entries
+    // "bucket" (round 5): the giant-filtered fold BUCKETED — both snapshot lookups of an edge in LDS (signed_bucket.h),
+    // for batches (past the sample) of at least "bucket_min" edges when the vote found a component; "bucket_levels":
+    // filter levels before the rest (1 or 2)
+    int bucket = 1;
+    u64 bucket_min = 1ull << 22;
+    int bucket_levels = 2;
+    gcc_forest* bk_scratch = nullptr;  // a CC forest of the same id range: its bucket storage (P1) only
+    u32* d_n2 = nullptr;               // 2 bits per id + the 8 counter words behind them
+    u64* d_lists = nullptr;            // the emit list and two slow lists
+    u64 list_cap = 0;                  // entries per list
+    u64 last_counts[4] = {0, 0, 0, 0}; // the last bucketed fold's emitted / slow entries per level (diagnostics)
     std::vector<u32> host_words;
     bool host_valid = false;
 };
@@ -458,6 +472,55 @@ static int signed_compress(gcc_signed* h) {
 }
 
 static int signed_fold_plain(gcc_signed* h, const u64* edges, u64 n);
+
+// The bucketed giant-filtered fold of the batch's rest (the snapshot and the vote made, a component found): gelly_cc.hip
+// gcc_internal_signed_bucket. It ends with the closing compress (deferred members are labelled from the bits).
+static int signed_fold_bucketed(gcc_signed* h, const u64* edges, u64 n, const u32* vote) {
+    const u64 nw = ((u64)h->cap + 15) / 16;
+    if (!h->bk_scratch) {
+        int rc = gcc_forest_create(h->device, h->cap, &h->bk_scratch);
+        if (rc) return rc;
+        HIP_TRY(hipMalloc((void**)&h->d_n2, (nw + 8) * sizeof(u32)));
+        HIP_TRY(hipMemsetAsync(h->d_n2, 0, (nw + 8) * sizeof(u32), h->stream));
+    }
+    if (h->list_cap < n) {
+        if (h->d_lists) {
+            HIP_TRY(hipStreamSynchronize(h->stream));
+            HIP_TRY(hipFree(h->d_lists));
+            h->d_lists = nullptr;
+        }
+        const u64 c = (n + 15) / 16 * 16;
+        HIP_TRY(hipMalloc((void**)&h->d_lists, 3 * c * sizeof(u64)));
+        h->list_cap = c;
+    }
+    GccSignedBucketArgs a{};
+    a.stream = h->stream;
+    a.word = h->d_word;
+    a.out = h->d_spare;
+    a.gbits = h->d_gbits;
+    a.n2 = h->d_n2;
+    a.vote = vote;
+    a.fail = h->d_fail;
+    a.edges = edges;
+    a.n = n;
+    a.cap = h->cap;
+    a.emit = h->d_lists;
+    a.slow0 = h->d_lists + h->list_cap;
+    a.slow1 = h->d_lists + 2 * h->list_cap;
+    a.ctr = h->d_n2 + nw;
+    a.levels = h->bucket_levels;
+    int rc = gcc_internal_signed_bucket(h->bk_scratch, &a);
+    if (rc) return rc;
+    std::memcpy(h->last_counts, a.counts, sizeof(a.counts));
+    if (const char* e = std::getenv("GELLY_BUCKET_STATS"); e && *e && *e != '0')
+        std::fprintf(stderr, "[signed-bucket] n=%llu level 1: emitted %llu slow %llu; level 2: emitted %llu slow %llu\n",
+                     (unsigned long long)n, (unsigned long long)a.counts[0], (unsigned long long)a.counts[1],
+                     (unsigned long long)a.counts[2], (unsigned long long)a.counts[3]);
+    std::swap(h->d_word, h->d_spare);  // the closing compress wrote the canonical words
+    h->compressed = true;
+    h->host_valid = false;
+    return GCC_OK;
+}
 
 // a batch of at least 2^22 edges and a quarter of the id range (the snapshot's O(ids) passes amortised): the
 // giant-filtered fold (above signed_vote_kernel)
@@ -476,6 +539,13 @@ static int signed_fold(gcc_signed* h, const u32* d_pairs, u64 n) {
     hipLaunchKernelGGL(signed_snapshot_kernel, dim3(grid_for_n(nw, kMaxGrid)), dim3(256), 0, h->stream, h->d_word, h->cap,
                        vote, min_count, h->d_gbits);
     HIP_TRY(hipGetLastError());
+    if (n > s && h->bucket && n - s >= h->bucket_min && h->cap <= (1u << 28) &&
+        ((reinterpret_cast<uintptr_t>(edges + s) & 15) == 0)) {
+        u32 hv[2];  // the vote: a component to filter against, or the plain fold (no bucketing for it)
+        HIP_TRY(hipMemcpyAsync(hv, vote, sizeof(hv), hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        if (hv[1] >= min_count) return signed_fold_bucketed(h, edges + s, n - s, vote);
+    }
     if (n > s && h->xcd && n - s >= h->xcd_min && ((reinterpret_cast<uintptr_t>(edges + s) & 15) == 0)) {
         // the split: capacities from a sample, chunked reservations, the overflow list after the parts
         const u64 m_edges = n - s;
@@ -583,6 +653,9 @@ int gcc_signed_destroy(gcc_signed* h) {
     if (h->d_split) (void)hipFree(h->d_split);
     if (h->d_xm) (void)hipFree(h->d_xm);
     if (h->d_stage) (void)hipFree(h->d_stage);
+    if (h->d_n2) (void)hipFree(h->d_n2);
+    if (h->d_lists) (void)hipFree(h->d_lists);
+    if (h->bk_scratch) (void)gcc_forest_destroy(h->bk_scratch);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
     return GCC_OK;
@@ -680,6 +753,14 @@ int gcc_signed_tune(gcc_signed* h, const char* key, double value) {
     } else if (k == "xcd_min") {
         CHECK_ARG(value >= 0, "xcd_min must be >= 0");
         h->xcd_min = (u64)value;
+    } else if (k == "bucket") {
+        h->bucket = value != 0;
+    } else if (k == "bucket_min") {
+        CHECK_ARG(value >= 0, "bucket_min must be >= 0");
+        h->bucket_min = (u64)value;
+    } else if (k == "bucket_levels") {
+        CHECK_ARG(value == 1 || value == 2, "bucket_levels must be 1 or 2");
+        h->bucket_levels = (int)value;
     } else if (k == "min_share") {
         CHECK_ARG(value > 0 && value <= 1, "min_share must be in (0, 1]");
         h->min_share = value;

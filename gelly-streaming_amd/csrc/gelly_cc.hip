@@ -1839,6 +1839,8 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
 }
 
 #include "bucket_fold.h"
+#include "signed_bucket.h"  // the signed forest's bucketed fold (gelly_bip.hip), reusing bucket_fold.h's P1
+#include "signed_bucket_api.h"
 
 static constexpr size_t slice_filter_lds(int per = 8, int vw = 4) {  // bucket_fold.h slice_filter_kernel's dynamic LDS
     return (bk::kSliceWords + bk::p2_tile(per, vw) + 10 * bk::kMaxVLists) * sizeof(u32) + bk::kMaxVLists * sizeof(u64) +
@@ -3276,6 +3278,109 @@ static int counts(gcc_forest* h, unsigned long long out[2]) {
     HIP_TRY(hipMemcpyAsync(out, h->d_counts, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
     return stream_sync_checked(h);
 }
+// P1 of the bucketed fold alone (layout + bucket_kernel), into f's bucket storage: n u64 pairs split by the FIRST id's
+// 2^19-id slice. For the signed forest's bucketed fold (signed_bucket.h), which treats P1 as a plain partition.
+static int bucketize(gcc_forest* f, const u64* edges, u64 n, u32** lo_out, bk::u16** hi_out) {
+    const u32 ns = bucket_slices(f);
+    if (!f->d_meta) HIP_TRY(hipMalloc((void**)&f->d_meta, sizeof(bk::Meta)));
+    const u32 p1_blocks = 2 * (u32)f->n_cu;
+    const u32 p2_blocks = std::min<u32>((u32)f->n_cu, bk::kMaxP2Blocks);
+    const u32 chunk = bk::chunk_entries(n, 0);
+    const u64 bk_S = bk::bk_entries(bk::storage_edges(n, ns, p1_blocks, bk::bk_aligned(n), chunk));
+    int rc = grow(f->d_bk, f->bk_cap_bytes, bk::bk_bytes(bk_S), f->stream);
+    if (!rc) rc = grow(f->d_ovf, f->ovf_cap, n / 8 + 65536, f->stream);
+    if (rc) return rc;
+    u32* bk_lo = reinterpret_cast<u32*>(f->d_bk);
+    bk::u16* bk_hi = reinterpret_cast<bk::u16*>(f->d_bk + 4 * bk_S);
+    const u32 ovf_cap = (u32)std::min<u64>(f->ovf_cap, 0xFFFFFFF0ull);
+    rc = launch_k(f, "sb_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, f->cap, f->d_meta,
+                  p1_blocks, p2_blocks, chunk);
+    if (!rc)
+        rc = ns > 256 ? launch_k(f, "sb_bucket", n, bk::bucket_kernel<1024, 12, 512>, dim3(f->n_cu), dim3(1024),
+                                 bk::p1_lds(1024, 12, 512), edges, n, ns, f->cap, f->d_meta, bk_lo, bk_hi, f->d_ovf,
+                                 ovf_cap, f->d_err, (u32*)nullptr)
+                      : launch_k(f, "sb_bucket", n, bk::bucket_kernel<1024, 16>, dim3(f->n_cu), dim3(1024),
+                                 bk::p1_lds(1024, 16), edges, n, ns, f->cap, f->d_meta, bk_lo, bk_hi, f->d_ovf, ovf_cap,
+                                 f->d_err, (u32*)nullptr);
+    *lo_out = bk_lo;
+    *hi_out = bk_hi;
+    return rc;
+}
+
+// The bucketed signed fold (signed_bucket.h's header comment): `levels` rounds of P1 + filter + P1 + check + join, the
+// rest, the closing compress into a->out. Synchronises twice per level (the emitted and slow counts size the next P1).
+int gcc_internal_signed_bucket(gcc_forest* f, GccSignedBucketArgs* a) {
+    DeviceGuard g(f->device);
+    f->stream = a->stream;
+    const u32 ns = bucket_slices(f);
+    const u32 nw16 = (u32)(((u64)a->cap + 15) / 16);
+    const u32 items = 4 * (u32)f->n_cu;
+    const u32 cps = std::max<u32>(1, (items + ns - 1) / ns);
+    const size_t lds = sb::kSliceW * sizeof(u32);
+    auto ovf_cap = [&]() -> u32 { return (u32)std::min<u64>(f->ovf_cap, 0xFFFFFFF0ull); };  // grows with the lists
+    int rc = GCC_OK;
+    const u64* src = a->edges;
+    u64 n = a->n;
+    u64* slow_out = a->slow0;
+    HIP_TRY(hipMemsetAsync(a->ctr, 0, 8 * sizeof(u32), f->stream));
+    for (int lv = 0; lv < std::max(1, std::min(2, a->levels)) && n >= 64 && !rc; ++lv) {
+        u32* lo;
+        bk::u16* hi;
+        rc = bucketize(f, src, n, &lo, &hi);
+        if (!rc) HIP_TRY(hipMemsetAsync(a->ctr, 0, 3 * sizeof(u32), f->stream));
+        if (!rc)
+            rc = launch_k(f, "sb_filter", n, sb::sb_filter_kernel, dim3(f->n_cu), dim3(sb::kBlock), lds, (const u32*)lo,
+                          (const bk::u16*)hi, (const bk::Meta*)f->d_meta, ns, cps, a->ctr, (const u32*)a->gbits, nw16,
+                          a->emit, slow_out, a->cap, f->d_err);
+        // the bucketing's overflow list (edges): the rest's rule now (exact at any time: deferred members are never
+        // united directly); a spill sets ctr[3] for the whole batch at the end
+        if (!rc)
+            rc = launch_k(f, "sb_rest", 0, sb::sb_rest_kernel, dim3(grid_for(std::max<u64>(1, ovf_cap()), 1024)), dim3(256), 0,
+                          a->word, (const u64*)f->d_ovf, (u64)ovf_cap(), (const u32*)&f->d_meta->ovf_cur, 0u,
+                          (const bk::Meta*)f->d_meta, a->gbits, a->vote, a->cap, a->fail, a->ctr);
+        if (rc) return rc;
+        u32 cnt[2];
+        HIP_TRY(hipMemcpyAsync(cnt, a->ctr + 1, sizeof(cnt), hipMemcpyDeviceToHost, f->stream));
+        rc = stream_sync_checked(f);
+        if (rc) return rc;
+        a->counts[2 * lv] = cnt[0];
+        a->counts[2 * lv + 1] = cnt[1];
+        if (cnt[0] >= 64) {  // the emitted pairs by v's slice, then checked / added with v's slice in LDS
+            rc = bucketize(f, a->emit, cnt[0], &lo, &hi);
+            if (!rc) HIP_TRY(hipMemsetAsync(a->ctr, 0, sizeof(u32), f->stream));
+            if (!rc)
+                rc = launch_k(f, "sb_check", cnt[0], sb::sb_check_kernel, dim3(f->n_cu), dim3(sb::kBlock), lds,
+                              (const u32*)lo, (const bk::u16*)hi, (const bk::Meta*)f->d_meta, ns, cps, a->ctr,
+                              (const u32*)a->gbits, nw16, a->n2, a->cap, a->fail, f->d_err);
+            if (!rc)
+                rc = launch_k(f, "sb_check_ovf", 0, sb::sb_check_list_kernel, dim3(grid_for(std::max<u64>(1, ovf_cap()), 1024)),
+                              dim3(256), 0, (const u64*)f->d_ovf, ovf_cap(), (const bk::Meta*)f->d_meta,
+                              (const u32*)a->gbits, a->n2, a->cap, a->fail, a->ctr);
+        } else if (cnt[0]) {  // a handful: against the global snapshot straight away
+            rc = launch_k(f, "sb_check_ovf", 0, sb::sb_check_list_kernel, dim3(1), dim3(256), 0, (const u64*)a->emit,
+                          (u32)cnt[0], (const bk::Meta*)nullptr, (const u32*)a->gbits, a->n2, a->cap, a->fail, a->ctr);
+        }
+        if (!rc)
+            rc = launch_k(f, "sb_join", 0, sb::sb_join_kernel, dim3(grid_for(nw16, kMaxGrid)), dim3(256), 0, a->word,
+                          a->gbits, a->n2, nw16, a->vote, a->fail);
+        src = slow_out;
+        n = cnt[1];
+        slow_out = slow_out == a->slow0 ? a->slow1 : a->slow0;
+    }
+    // the last level's slow edges, then (only after a spill: ctr[3]) the whole batch again
+    if (!rc && n)
+        rc = launch_k(f, "sb_rest", n, sb::sb_rest_kernel, dim3(grid_for(n, kMaxGrid)), dim3(256), 0, a->word, src, n,
+                      (const u32*)nullptr, 0u, (const bk::Meta*)nullptr, a->gbits, a->vote, a->cap, a->fail, a->ctr);
+    if (!rc)
+        rc = launch_k(f, "sb_rest", 0, sb::sb_rest_kernel, dim3(grid_for(a->n, kMaxGrid)), dim3(256), 0, a->word,
+                      a->edges, a->n, (const u32*)nullptr, 1u, (const bk::Meta*)nullptr, a->gbits, a->vote, a->cap,
+                      a->fail, a->ctr);
+    if (!rc)
+        rc = launch_k(f, "sb_compress", 0, sb::sb_compress_kernel, dim3(grid_for(a->cap, kMaxGrid)), dim3(256), 0, a->word,
+                      a->out, a->cap, (const u32*)a->gbits, a->vote);
+    return rc;
+}
+
 // ------------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------------
@@ -3402,6 +3507,8 @@ static int set_lds_attrs_impl() {
         {(const void*)compress_inc_kernel<false, true>, (int)(gcc::kBloomBits / 8)},
         {(const void*)compress_inc_kernel<true, true>, (int)(gcc::kBloomBits / 8)},
         {(const void*)compress_pipe_kernel, (int)(gcc::kBloomBits / 8)},
+        {(const void*)sb::sb_filter_kernel, (int)(sb::kSliceW * sizeof(u32))},
+        {(const void*)sb::sb_check_kernel, (int)(sb::kSliceW * sizeof(u32))},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, false>, filtered},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true, false>, filtered},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, true>, filtered},

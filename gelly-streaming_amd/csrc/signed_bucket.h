@@ -1,0 +1,344 @@
+// signed_bucket.h — the BUCKETED giant-filtered fold of the signed forest (BipartitenessCheck's summary, gelly_bip.hip),
+// round 5. Included by gelly_cc.hip after bucket_fold.h, whose P1 (bucket_kernel: the batch split
+// by the first id's 2^19-id slice into 6-B entries) it reuses as a plain partition; the host side is
+// gcc_internal_signed_bucket in gelly_cc.hip, called by gelly_bip.hip's signed_fold.
+//
+// The giant-filtered fold (gelly_bip.hip signed_fold_giant_kernel) looks up two 2-bit snapshot entries per edge — in
+// C (the voted component), and the parity to C's root r — in a 16 MiB array at 2^26 ids, beyond an XCD's L2: random
+// 64-B line fetches bound it (1.7 misses per edge). Here both lookups find their slice of the snapshot in LDS:
+//   sb_filter_kernel   per source-slice bucket, the slice's 2 bits per id in LDS (128 KiB): u in C -> the pair
+//                      (v, parity(u) ^ 1) joins the EMIT list (v must carry that parity); else the edge joins the SLOW
+//                      list with its ends swapped (block-aggregated appends: one global add per list per 4K entries)
+//   bucket_kernel      the emit list split by v's slice (the same P1)
+//   sb_check_kernel    per target-slice bucket, the slice in LDS: v in C -> its parity must be the pair's, else the
+//                      batch has an odd cycle (fail); v not in C -> v joins the block's LDS copy with that parity (a
+//                      lane that finds it added with the other parity: fail); at the end of its items a block ORs
+//                      its new members into N2, 2 bits per id: "reached with parity 0", "with parity 1"
+//   sb_join_kernel     C |= N2 (both parities: fail); a new member already seen in the forest (the sample's fold made
+//                      it seen in another tree), or below r, is united with r with its parity; the others stay
+//                      UNSEEN in the forest — DEFERRED, as the CC fold's N (bucket_join_kernel)
+// then the same again over the slow list against C | N (a second level) — by the edges' OTHER ends: a bipartite
+// stream's sources and targets can be disjoint sets (to_bipartite: even -> odd ids), and N holds targets — and the
+// remaining edges by
+//   sb_rest_kernel     the giant kernel's rule with deferred members: an edge with one end x outside C unites x with
+//                      r (never with the deferred end itself); neither end in C: the signed union
+//   sb_compress_kernel the closing compress: a member of C is labelled (root(r) << 1) | (its parity ^ r's parity to
+//                      root(r)) straight from the bits (the deferred ones need no forest entry); the others by find.
+// Every parity a bit holds is implied by edges of the batch (the snapshot's by the forest, the rest by an edge from a
+// member), so two bits that disagree are an odd cycle: the summary fails, as the reference's Candidates.merge does at
+// the edge that closes it (…/summaries/Candidates.java:77-139; a failed summary's words are not part of the contract).
+#pragma once
+
+#include "signed_uf.h"
+
+namespace sb {
+
+using bk::kSliceBits;
+constexpr u32 kSliceW = (1u << kSliceBits) / 16;  // 2-bit words of a slice: 32768 (128 KiB of LDS)
+constexpr int kBlock = 1024;
+constexpr u32 kMask2 = 0x55555555u;               // bit 2j of every 2-bit pair
+
+__device__ __forceinline__ u32 pair2(u32 w, u32 x) { return (w >> (2 * (x & 15))) & 3u; }
+
+// the slice's 2-bit words of the snapshot into LDS (beyond the id range: zero)
+__device__ __forceinline__ void load_slice2(u32* s, const u32* __restrict__ g, u32 sl, u32 nw16) {
+    const u32 w0 = sl * kSliceW;
+    for (u32 w = threadIdx.x; w < kSliceW; w += kBlock) s[w] = w0 + w < nw16 ? g[w0 + w] : 0u;
+}
+
+// Block-aggregated appends of this round's entries (bit c of m: entry c of the lane's 4) to a global list: a wave's
+// count by ballots, the block's by one scan in LDS, ONE global add per list per round.
+struct Appender {
+    u32* s_wc;    // [16 waves][2 lists]
+    u32* s_base;  // [2]
+};
+__device__ __forceinline__ void append2(const Appender& ap, u32* cursors, u64* l0, u64* l1, u32 m0, u32 m1,
+                                        const u64 (&e0)[4], const u64 (&e1)[4]) {
+    const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u32 c0 = 0, c1 = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        c0 += (u32)__popcll(__ballot((m0 >> c) & 1u));
+        c1 += (u32)__popcll(__ballot((m1 >> c) & 1u));
+    }
+    if (lane == 0) {
+        ap.s_wc[2 * wv] = c0;
+        ap.s_wc[2 * wv + 1] = c1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        u32 tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const u32 c = ap.s_wc[2 * w + threadIdx.x];
+            ap.s_wc[2 * w + threadIdx.x] = tot;
+            tot += c;
+        }
+        ap.s_base[threadIdx.x] = tot ? atomicAdd(&cursors[threadIdx.x], tot) : 0u;
+    }
+    __syncthreads();
+    u32 p0 = ap.s_base[0] + ap.s_wc[2 * wv], p1 = ap.s_base[1] + ap.s_wc[2 * wv + 1];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const u64 b0 = __ballot((m0 >> c) & 1u), b1 = __ballot((m1 >> c) & 1u);
+        const u32 r0 = __builtin_amdgcn_mbcnt_hi((u32)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((u32)b0, 0u));
+        const u32 r1 = __builtin_amdgcn_mbcnt_hi((u32)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((u32)b1, 0u));
+        if ((m0 >> c) & 1u) l0[p0 + r0] = e0[c];
+        if ((m1 >> c) & 1u) l1[p1 + r1] = e1[c];
+        p0 += (u32)__popcll(b0);
+        p1 += (u32)__popcll(b1);
+    }
+}
+
+// Work items: (slice, part) of the buckets, dequeued from ctr[0]. Every round of a block takes 4 entries per lane.
+// ctr[1] / ctr[2]: the emit / slow cursors.
+__global__ __launch_bounds__(kBlock) void sb_filter_kernel(const u32* __restrict__ bk_lo, const bk::u16* __restrict__ bk_hi,
+                                                           const bk::Meta* __restrict__ m, u32 ns, u32 cps,
+                                                           u32* __restrict__ ctr, const u32* __restrict__ gbits, u32 nw16,
+                                                           u64* __restrict__ emit, u64* __restrict__ slow, u32 cap,
+                                                           u32* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) u32 s_bits[];  // kSliceW
+    __shared__ u32 s_item, s_wc[2 * (kBlock / 64)], s_base[2];
+    const Appender ap{s_wc, s_base};
+    typedef u32 u4 __attribute__((ext_vector_type(4)));
+    const u32 n_items = ns * cps;
+    u32 cur = 0xFFFFFFFFu;
+    while (true) {
+        __syncthreads();
+        if (threadIdx.x == 0) s_item = atomicAdd(&ctr[0], 1u);
+        __syncthreads();
+        const u32 item = s_item;
+        if (item >= n_items) break;
+        const u32 sl = item / cps;
+        const u64 len = m->bk_cur[sl] < m->bk_cap[sl] ? m->bk_cur[sl] : m->bk_cap[sl];
+        u64 lo, hi;
+        bk::item_range(len, item % cps, cps, lo, hi);
+        if (lo >= hi) continue;
+        if (sl != cur) {
+            load_slice2(s_bits, gbits, sl, nw16);
+            cur = sl;
+            __syncthreads();
+        }
+        const u32 sbase = sl << kSliceBits;
+        const u64 base = m->bk_base[sl];
+        const u64 g0 = lo / 4, g1 = (hi + 3) / 4;  // 4-entry groups (bases: 16-entry multiples)
+        for (u64 gb = g0; gb < g1; gb += kBlock) {  // block-uniform
+            const u64 g = gb + threadIdx.x;
+            u32 em = 0, smk = 0, bad = 0;
+            u64 ev[4] = {0, 0, 0, 0}, sv[4] = {0, 0, 0, 0};
+            if (g < g1) {
+                const u4 l4 = *reinterpret_cast<const u4*>(bk_lo + base + 4 * g);
+                const u64 h4 = *reinterpret_cast<const u64*>(bk_hi + base + 4 * g);
+                const u32 lv[4] = {l4.x, l4.y, l4.z, l4.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    u32 u, v;
+                    const u64 e = 4 * g + c;
+                    if (!bk::bk_decode(lv[c], (bk::u16)(h4 >> (16 * c)), sbase, u, v) || e < lo || e >= hi) continue;
+                    if (v >= cap) {
+                        bad = 1;
+                        continue;
+                    }
+                    const u32 b = pair2(s_bits[(u - sbase) >> 4], u);
+                    if (b & 1u) {  // u in C: v must take the other parity (a self loop in C: nothing to do)
+                        if (u != v) {
+                            ev[c] = (u64)v | ((u64)(((b >> 1) & 1u) ^ 1u) << 32);
+                            em |= 1u << c;
+                        }
+                    } else {  // slow: listed with its ends SWAPPED, so that the next level looks at the other end
+                        sv[c] = ((u64)u << 32) | v;
+                        smk |= 1u << c;
+                    }
+                }
+            }
+            if (bad) bk::flag_err(err, bk::kErrP2);
+            append2(ap, ctr + 1, emit, slow, em, smk, ev, sv);
+        }
+    }
+}
+
+// The new members of the block's slice copy (set in LDS, not in the snapshot) into N2: bit 2j "reached with parity
+// 0", bit 2j + 1 "with parity 1" (memory-side ORs; the join reads them in a later kernel)
+__device__ __forceinline__ void flush_slice2(const u32* s, const u32* __restrict__ gbits, u32* __restrict__ n2, u32 sl,
+                                             u32 nw16) {
+    const u32 w0 = sl * kSliceW;
+    for (u32 w = threadIdx.x; w < kSliceW && w0 + w < nw16; w += kBlock) {
+        const u32 lw = s[w];
+        const u32 nm = lw & ~gbits[w0 + w] & kMask2;  // members this block added
+        if (!nm) continue;
+        const u32 p1 = (lw >> 1) & nm;
+        atomicOr(&n2[w0 + w], (nm & ~p1) | (p1 << 1));
+    }
+}
+
+// Work items over the emit list's buckets (entries: v, parity p): see the header comment. ctr[0]: the item counter.
+__global__ __launch_bounds__(kBlock) void sb_check_kernel(const u32* __restrict__ bk_lo, const bk::u16* __restrict__ bk_hi,
+                                                          const bk::Meta* __restrict__ m, u32 ns, u32 cps,
+                                                          u32* __restrict__ ctr, const u32* __restrict__ gbits, u32 nw16,
+                                                          u32* __restrict__ n2, u32 cap, u32* __restrict__ fail,
+                                                          u32* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) u32 s_bits[];  // kSliceW
+    __shared__ u32 s_item;
+    typedef u32 u4 __attribute__((ext_vector_type(4)));
+    const u32 n_items = ns * cps;
+    u32 cur = 0xFFFFFFFFu;
+    u32 odd = 0;
+    while (true) {
+        __syncthreads();
+        if (threadIdx.x == 0) s_item = atomicAdd(&ctr[0], 1u);
+        __syncthreads();
+        const u32 item = s_item;
+        if (item >= n_items) break;
+        const u32 sl = item / cps;
+        const u64 len = m->bk_cur[sl] < m->bk_cap[sl] ? m->bk_cur[sl] : m->bk_cap[sl];
+        u64 lo, hi;
+        bk::item_range(len, item % cps, cps, lo, hi);
+        if (lo >= hi) continue;
+        if (sl != cur) {
+            if (cur != 0xFFFFFFFFu) flush_slice2(s_bits, gbits, n2, cur, nw16);
+            __syncthreads();
+            load_slice2(s_bits, gbits, sl, nw16);
+            cur = sl;
+            __syncthreads();
+        }
+        const u32 sbase = sl << kSliceBits;
+        const u64 base = m->bk_base[sl];
+        const u64 g0 = lo / 4, g1 = (hi + 3) / 4;
+        for (u64 g = g0 + threadIdx.x; g < g1; g += kBlock) {
+            const u4 l4 = *reinterpret_cast<const u4*>(bk_lo + base + 4 * g);
+            const u64 h4 = *reinterpret_cast<const u64*>(bk_hi + base + 4 * g);
+            const u32 lv[4] = {l4.x, l4.y, l4.z, l4.w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                u32 x, p;
+                const u64 e = 4 * g + c;
+                if (!bk::bk_decode(lv[c], (bk::u16)(h4 >> (16 * c)), sbase, x, p) || e < lo || e >= hi) continue;
+                if (x >= cap || p > 1u) {
+                    bk::flag_err(err, bk::kErrP2);
+                    continue;
+                }
+                const u32 xl = x - sbase, sh = 2 * (xl & 15);
+                const u32 b = (s_bits[xl >> 4] >> sh) & 3u;
+                if (b & 1u) {  // a member (of C, or added by this block): the parities must agree
+                    odd |= (b >> 1) != p;
+                } else {
+                    const u32 o = (atomicOr(&s_bits[xl >> 4], (1u | p << 1) << sh) >> sh) & 3u;
+                    odd |= (o & 1u) && (o >> 1) != p;  // another lane added it with the other parity
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (cur != 0xFFFFFFFFu) flush_slice2(s_bits, gbits, n2, cur, nw16);
+    if (odd) suf::st(fail, 1u);
+}
+
+// A list of pairs (v, p) checked against the GLOBAL snapshot, new members straight into N2: the emit bucketing's
+// overflow list (m: its count is m->ovf_cur, and a spill — P1's overflow list overflowed, entries lost — sets ctr[3]: the
+// final sb_rest_kernel pass then takes the whole batch again), or a short emit list that was not worth a P1.
+__global__ __launch_bounds__(256) void sb_check_list_kernel(const u64* __restrict__ list, u32 n, const bk::Meta* __restrict__ m,
+                                                            const u32* __restrict__ gbits, u32* __restrict__ n2, u32 cap,
+                                                            u32* __restrict__ fail, u32* __restrict__ ctr) {
+    if (m) {
+        if (blockIdx.x == 0 && threadIdx.x == 0 && m->spill) ctr[3] = 1u;
+        n = m->ovf_cur < n ? m->ovf_cur : n;
+    }
+    for (u32 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const u64 e = list[i];
+        const u32 x = (u32)e, p = (u32)(e >> 32);
+        if (x >= cap || p > 1u) continue;
+        const u32 b = pair2(gbits[x >> 4], x);
+        if (b & 1u) {
+            if ((b >> 1) != p) suf::st(fail, 1u);
+        } else {
+            atomicOr(&n2[x >> 4], 1u << (2 * (x & 15) + p));
+        }
+    }
+}
+
+// C |= N2 (see the header comment). r = vote[0], C's root at the snapshot. N2 is cleared for the next level.
+__global__ __launch_bounds__(256) void sb_join_kernel(u32* __restrict__ word, u32* __restrict__ gbits, u32* __restrict__ n2,
+                                                      u32 nw16, const u32* __restrict__ vote, u32* __restrict__ fail) {
+    const u32 r = vote[0];
+    for (u32 w = blockIdx.x * 256 + threadIdx.x; w < nw16; w += gridDim.x * 256) {
+        const u32 h = n2[w];
+        if (!h) continue;
+        atomicExch(&n2[w], 0u);  // memory-side: the next level's ORs follow in later kernels
+        const u32 h0 = h & kMask2, h1 = (h >> 1) & kMask2;
+        if (h0 & h1) suf::st(fail, 1u);  // reached with both parities: an odd cycle
+        const u32 nm = h0 | h1;
+        atomicOr(&gbits[w], nm | (h1 << 1));
+        for (u32 d = nm; d; d &= d - 1) {
+            const u32 j = (u32)__builtin_ctz(d) >> 1, x = w * 16 + j;
+            if (x < r || suf::ld(&word[x]) != suf::kUnseen) suf::unite(word, x, r, (h1 >> (2 * j)) & 1u, fail);
+        }
+    }
+}
+
+// The remaining edges (the last level's slow list, every source bucketing's overflow list — n_dev: its count, and
+// spill_meta: a spill there sets ctr[3]; the whole batch again when a bucketing spilled: `needs_spill`, then only when
+// ctr[3] is set) by the giant kernel's rule, deferred-safe.
+__global__ __launch_bounds__(256) void sb_rest_kernel(u32* __restrict__ word, const u64* __restrict__ edges, u64 n,
+                                                      const u32* __restrict__ n_dev, u32 needs_spill,
+                                                      const bk::Meta* __restrict__ spill_meta, u32* __restrict__ gbits,
+                                                      const u32* __restrict__ vote, u32 cap, u32* __restrict__ fail,
+                                                      u32* __restrict__ ctr) {
+    if (needs_spill && !ctr[3]) return;
+    if (spill_meta && blockIdx.x == 0 && threadIdx.x == 0 && spill_meta->spill) ctr[3] = 1u;
+    if (n_dev) n = *n_dev < n ? *n_dev : n;
+    const u32 r = vote[0];
+    const u64 stride = (u64)gridDim.x * 256;
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const u64 e = edges[i];
+        if (e == ~0ull) continue;
+        const u32 u = (u32)e, v = (u32)(e >> 32);
+        if (u >= cap || v >= cap) continue;
+        const u32 bu = pair2(suf::ld(&gbits[u >> 4]), u), bv = pair2(suf::ld(&gbits[v >> 4]), v);
+        if (bu & bv & 1u) {  // both in C: a check
+            if (u != v && !((bu ^ bv) & 2u)) suf::st(fail, 1u);
+            continue;
+        }
+        if ((bu ^ bv) & 1u) {  // one end in C: the other end x joins C under r, with the parity the edge implies
+            const u32 x = (bu & 1u) ? v : u, px = ((((bu & 1u) ? bu : bv) >> 1) & 1u) ^ 1u;
+            atomicOr(&gbits[x >> 4], (1u | px << 1) << (2 * (x & 15)));
+            if (!(r < x && suf::ld(&word[x]) == suf::kUnseen &&
+                  suf::cas(&word[x], suf::kUnseen, (r << 1) | px) == suf::kUnseen))
+                suf::unite(word, x, r, px, fail);
+            continue;
+        }
+        suf::unite(word, u, v, 1u, fail);
+    }
+}
+
+// The closing compress (out of place): C's members from the bits, the rest by find (gelly_bip.hip
+// signed_compress_kernel's rule).
+__global__ __launch_bounds__(256) void sb_compress_kernel(u32* __restrict__ word, u32* __restrict__ out, u32 n,
+                                                          const u32* __restrict__ gbits, const u32* __restrict__ vote) {
+    __shared__ u32 s_rf, s_pr;
+    if (threadIdx.x == 0) {
+        const u32 r = vote[0];
+        u32 pr = 0;
+        s_rf = suf::find_ro(word, r, suf::ld(&word[r]), pr);
+        s_pr = pr;
+    }
+    __syncthreads();
+    const u32 rf = s_rf, pr = s_pr;
+    const u64 stride = (u64)gridDim.x * 256;
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const u32 v = (u32)i;
+        const u32 b = pair2(gbits[v >> 4], v);
+        if (b & 1u) {
+            out[v] = (rf << 1) | (((b >> 1) & 1u) ^ pr);
+            continue;
+        }
+        const u32 w = word[v];
+        if (w == suf::kUnseen || suf::parent_of(w) == v) {
+            out[v] = w;
+            continue;
+        }
+        u32 par;
+        const u32 root = suf::find_ro(word, v, w, par);
+        out[v] = (root << 1) | par;
+    }
+}
+
+}  // namespace sb

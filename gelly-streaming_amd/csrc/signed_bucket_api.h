@@ -1,0 +1,30 @@
+// signed_bucket_api.h — internal (not part of the C ABI): the bucketed signed fold, implemented in gelly_cc.hip next
+// to the CC forest's bucketed fold whose P1 it reuses (kernels: signed_bucket.h), called by gelly_bip.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+struct gcc_forest;
+
+struct GccSignedBucketArgs {
+    hipStream_t stream;
+    uint32_t* word;         // the signed forest
+    uint32_t* out;          // the closing compress's output (the caller swaps it in)
+    uint32_t* gbits;        // the snapshot: 2 bits per id (member, parity to r), grown by the fold
+    uint32_t* n2;           // scratch: 2 bits per id (reached with parity 0 / 1), zero before and after
+    const uint32_t* vote;   // vote[0] = r, C's root at the snapshot
+    uint32_t* fail;         // the forest's fail word
+    const uint64_t* edges;  // the batch (u64 pairs, 16-B aligned)
+    uint64_t n;
+    uint32_t cap;
+    uint64_t* emit;         // scratch lists of at least n entries each
+    uint64_t* slow0;
+    uint64_t* slow1;
+    uint32_t* ctr;          // scratch: 8 device words
+    int levels;             // filter levels (1 or 2) before the rest
+    uint64_t counts[4];     // out: emitted and slow entries of level 1, of level 2 (diagnostics)
+};
+
+// gcc status; `scratch` = a CC forest of the same id range, used for its bucket storage only (gcc_forest_create)
+int gcc_internal_signed_bucket(gcc_forest* scratch, GccSignedBucketArgs* a);

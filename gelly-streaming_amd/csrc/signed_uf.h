@@ -63,6 +63,26 @@ SUF_HD u32 find(u32* word, u32 x, u32 wx, u32& par) {
     return cur;
 }
 
+// find without path splitting (read-only): a compress that writes its labels into the other buffer (the late-store
+// model of the CC forest, DESIGN.md §3: a split store into the old buffer could land over the labels written into it
+// when the buffers swap back)
+SUF_HD u32 find_ro(const u32* word, u32 x, u32 wx, u32& par) {
+    u32 acc = parity_of(wx), cur = parent_of(wx);
+    if (cur >= x) {
+        par = 0;
+        return x;
+    }
+    while (true) {
+        const u32 wc = ld(&word[cur]);
+        const u32 nxt = parent_of(wc);
+        if (nxt >= cur) break;
+        acc ^= parity_of(wc);
+        cur = nxt;
+    }
+    par = acc;
+    return cur;
+}
+
 // makeSet on first sight: the observed word of v, v made a root if it was unseen
 SUF_HD u32 seen(u32* word, u32 v) {
     u32 w = ld(&word[v]);

@@ -152,7 +152,8 @@ class Candidates:
         call("gcc_signed_set_stream", self.handle, c_void_p(hip_stream or 0), 1 if hip_stream is None else 0)
 
     def tune(self, **knobs) -> "Candidates":
-        """Speed-only knobs of the signed fold (gcc_signed_tune): giant, sample_shift, min_share."""
+        """Speed-only knobs of the signed fold (gcc_signed_tune): giant, sample_shift, min_share, unroll, xcd, xcd_min,
+        bucket, bucket_min, bucket_levels."""
         for k, v in knobs.items():
             call("gcc_signed_tune", self.handle, k.encode(), float(v))
         return self

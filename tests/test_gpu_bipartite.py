@@ -164,14 +164,15 @@ def test_bench_streams_full_size(golden):
     c.close()
 
 
-@pytest.mark.parametrize("giant,xcd", [(1, 1), (1, 0), (0, 0)])
+@pytest.mark.parametrize("giant,xcd,bucket", [(1, 1, 0), (1, 0, 0), (0, 0, 0), (1, 0, 1)])
 @pytest.mark.parametrize("odd", [False, True])
-def test_kron_hubs_vs_oracle(odd, giant, xcd):
+def test_kron_hubs_vs_oracle(odd, giant, xcd, bucket):
     """A kron stream mapped bipartite (hubs: contended roots), 3 windows, every window's words vs the oracle. Window
     1 (6M edges over 2^18 ids) takes the giant-filtered fold (gcc_signed_tune giant = 1, the default) — over the batch
-    split by source part, one part per XCD (xcd = 1, forced below its 2^25-edge default by xcd_min), or not — or the
-    plain one (giant = 0); with one odd edge between two hubs' side the summary fails in that window (inside the giant:
-    the parity-bit check), and the next window's fold stops at once."""
+    split by source part, one part per XCD (xcd = 1, forced below its 2^25-edge default by xcd_min), bucketed by the
+    ids' slices (bucket = 1, the default since round 5; one slice at 2^18 ids), or neither — or the plain one
+    (giant = 0); with one odd edge between two hubs' side the summary fails in that window (inside the giant: the
+    parity-bit check), and the next window's fold stops at once."""
     import torch
 
     cfg = G.scaled(G.CONFIGS["c4_kron26"], scale=18, n_edges=1 << 23)
@@ -183,12 +184,42 @@ def test_kron_hubs_vs_oracle(odd, giant, xcd):
     want = orc.bip_stream(pairs, starts, V, partitions=2)
     assert want["success"][0] and (want["success"][1] != odd)  # the odd edge closes a cycle in window 1
     d = torch.from_numpy(pairs.reshape(-1).view(np.int32)).cuda()
-    c = Candidates(V).tune(giant=giant, xcd=xcd, xcd_min=0)
+    c = Candidates(V).tune(giant=giant, xcd=xcd, xcd_min=0, bucket=bucket)
     for w in range(len(starts) - 1):
         c.fold_device(d.data_ptr() + 8 * starts[w], starts[w + 1] - starts[w])
         assert c.getSuccess() == bool(want["success"][w]), w
         if want["success"][w]:
             assert np.array_equal(c.words(), want["words"][w]), w
+    c.close()
+
+
+@pytest.mark.parametrize("odd", [False, True])
+@pytest.mark.parametrize("knobs", [{}, {"bucket_levels": 1}, {"sample_shift": 12}])
+def test_bucketed_fold_many_slices(odd, knobs):
+    """The bucketed signed fold (round 5) over 2^22 ids (8 slices of 2^19), a kron stream mapped bipartite: the same
+    words as the unbucketed giant kernel and the oracle's success flag; with one odd edge (two even hub ids) placed
+    late in the batch, the summary fails. A tiny sample (sample_shift 12: the snapshot holds a small part of the
+    giant) sends most edges through the second level and the rest."""
+    import torch
+
+    cfg = G.scaled(G.CONFIGS["c4_kron26"], scale=22, n_edges=1 << 23)
+    E, V = cfg.info()
+    pairs = G.to_bipartite(G.generate_host(cfg))
+    if odd:
+        pairs[(7 * E) // 8] = [pairs[0, 0], pairs[1, 0]]
+    d = torch.from_numpy(pairs.reshape(-1).view(np.int32)).cuda()
+    ref = Candidates(V).tune(bucket=0)
+    ref.fold_device(d.data_ptr(), E)
+    assert ref.getSuccess() != odd
+    c = Candidates(V).tune(**knobs)
+    c.fold_device(d.data_ptr(), E)
+    assert c.getSuccess() != odd
+    if not odd:
+        assert np.array_equal(c.words(), ref.words())
+        # a second batch into the same forest (the bucketed fold's words are canonical: a compressed forest)
+        c.fold_device(d.data_ptr(), E // 2)
+        assert c.getSuccess() and np.array_equal(c.words(), ref.words())
+    ref.close()
     c.close()
 
 
@@ -212,7 +243,8 @@ def test_giant_fold_knobs_and_no_dominant_component():
         ref.close()
         for knobs in ({}, {"sample_shift": 1}, {"sample_shift": 10}, {"min_share": 1.0}, {"min_share": 0.001},
                       {"unroll": 1}, {"unroll": 8}, {"xcd": 1, "xcd_min": 0}, {"xcd": 1, "xcd_min": 0, "min_share": 1.0},
-                      {"xcd": 1, "xcd_min": 0, "sample_shift": 10}, {"xcd": 1}):
+                      {"xcd": 1, "xcd_min": 0, "sample_shift": 10}, {"xcd": 1}, {"bucket": 0}, {"bucket_levels": 1},
+                      {"bucket_min": 0, "sample_shift": 10}, {"min_share": 0.001, "bucket_levels": 1}):
             c = Candidates(V).tune(**knobs)
             c.fold_device(d.data_ptr(), E)
             assert c.getSuccess() and np.array_equal(c.words(), want), (cfg.name, knobs)
