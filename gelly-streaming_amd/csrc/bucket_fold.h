@@ -71,6 +71,7 @@ struct Meta {
     u32 ring_used;               // FINAL P2 united some slow edges itself (its region was full): see bucket_join_kernel
     u32 chunk;                   // entries per chunk reservation (chunk_entries)
     u32 slow_cnt[kMaxP2Blocks];  // FINAL P2: slow edges (source not in C) each block listed in its own region
+    u64 n_list;                  // the batch size when the layout took it from the device (bucket_kernel: n = ~0)
 };
 constexpr u32 kVlPasses = 8;  // Meta::vl_cur: seeding levels 0..5, FINAL (6), the second level (7)
 constexpr u32 kVlFinal = 6, kVlLevel2 = 7;
@@ -268,25 +269,30 @@ __device__ __forceinline__ void block_prefix(const u32* cap, u64* base, u32 ns, 
     __syncthreads();
 }
 
+// n_dev / exact (the signed forest's bucketed fold, signed_bucket.h): the batch's size from the device (a list a
+// kernel appended; bucket_kernel then takes n = ~0 and reads m->n_list) and its exact per-bucket counts, no sample.
 __global__ __launch_bounds__(1024) void bucket_layout_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                               Meta* __restrict__ m, u32 bk_blocks, u32 vl_blocks,
-                                                              u32 chunk) {
+                                                              u32 chunk, const u32* __restrict__ n_dev,
+                                                              const u32* __restrict__ exact) {
     trace_start(kTrBkLayout);
     __shared__ u32 s_cu[kMaxBuckets], s_cv[kMaxVLists];
     __shared__ u64 s_scan[1024];
     const u32 nvs = vslices(cap);
+    if (n_dev) n = *n_dev < n ? *n_dev : n;
     for (u32 s = threadIdx.x; s < ns; s += 1024) {
-        s_cu[s] = 0;
+        s_cu[s] = exact ? exact[s] : 0u;
         if (s < nvs) s_cv[s] = 0;
     }
+    if (threadIdx.x == 0) m->n_list = n;
     __syncthreads();
-    const u64 n_smp = n < kSample ? n : kSample;
+    const u64 n_smp = exact ? n : n < kSample ? n : kSample;
     // the sample: kSample / 1024 = 64 runs of 1024 CONSECUTIVE edges spread evenly over the batch (coalesced, 64
     // pages; single edges kSample apart touched 64K pages and took this one block 0.12 ms on C4), 32 loads in
     // flight per thread (64 would spill)
     constexpr u32 kPer = kSample / 1024, kBatch = 32;
     const u64 run_stride = n / kPer;  // >= 1024 whenever n >= kSample; below that the sample is the batch
-    for (u32 b = 0; b < kPer; b += kBatch) {
+    for (u32 b = 0; b < (exact ? 0u : kPer); b += kBatch) {
         u64 e[kBatch];
 #pragma unroll
         for (u32 i = 0; i < kBatch; ++i) {
@@ -379,6 +385,7 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
                                                           u16* __restrict__ bk_hi, u64* __restrict__ ovf, u32 ovf_cap,
                                                           u32* __restrict__ err, u32* __restrict__ reset) {
     trace_start(kTrBkP1);
+    if (n == ~0ull) n = m->n_list;  // the layout took it from the device
     GCC_BT(0, 0);
     // the tile in bucket order: dynamic LDS (p1_lds: P1B * P1P + 3 MAXB u64, 66 / 130 KiB), set up like every
     // kernel's LDS beyond 64 KiB (gelly_cc.hip set_lds_attrs_impl); the per-bucket state below is static (MAXB >= ns)

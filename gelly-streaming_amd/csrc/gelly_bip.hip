@@ -114,26 +114,31 @@ __global__ __launch_bounds__(1024) void signed_vote_kernel(u32* __restrict__ wor
 }
 
 // 2 bits per id, 16 ids per word: bit 2j = id 16w+j in the voted root's component, bit 2j+1 = its parity to the root.
-// No component when the vote's share is below 1/min_share_inv of the samples (a batch without a dominant one).
+// No component when the vote's share is below 1/min_share_inv of the samples (a batch without a dominant one). One id
+// per lane (coalesced plain loads: the sample fold has completed), 16 lanes' bits OR-ed into a word by shuffles
+// (round 5: a lane per word read its 16 ids with 16 coherent loads 64 B apart: 239 us at 2^26 ids).
 __global__ __launch_bounds__(256) void signed_snapshot_kernel(u32* __restrict__ word, u32 n, const u32* __restrict__ vote,
                                                              u32 min_count, u32* __restrict__ gbits) {
     const bool on = vote[1] >= min_count;
     const u32 r = vote[0];
     const u32 nw = (n + 15) / 16;
-    for (u32 wi = blockIdx.x * 256 + threadIdx.x; wi < nw; wi += gridDim.x * 256) {
+    const u64 ids = (u64)nw * 16;
+    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i - threadIdx.x % 64 < ids; i += (u64)gridDim.x * 256) {
+        const u32 v = (u32)i;  // whole waves iterate together (the shuffles): ids past the range contribute nothing
         u32 b = 0;
-        if (on) {
-            for (u32 j = 0; j < 16; ++j) {
-                const u32 v = wi * 16 + j;
-                if (v >= n) break;
-                const u32 w = suf::ld(&word[v]);
-                if (w == kUnseen) continue;
+        if (on && i < n) {
+            const u32 w = word[v];
+            if (w != kUnseen) {
                 u32 par = 0;
                 const u32 root = sw_parent(w) == v ? v : sfind(word, v, w, par);
-                if (root == r) b |= (1u | par << 1) << (2 * j);
+                if (root == r) b = (1u | par << 1) << (2 * (v & 15));
             }
         }
-        gbits[wi] = b;
+        b |= __shfl_xor(b, 1, 64);
+        b |= __shfl_xor(b, 2, 64);
+        b |= __shfl_xor(b, 4, 64);
+        b |= __shfl_xor(b, 8, 64);
+        if ((v & 15) == 0 && i < ids) gbits[v >> 4] = b;
     }
 }
 
@@ -480,7 +485,7 @@ static int signed_fold_bucketed(gcc_signed* h, const u64* edges, u64 n, const u3
     if (!h->bk_scratch) {
         int rc = gcc_forest_create(h->device, h->cap, &h->bk_scratch);
         if (rc) return rc;
-        HIP_TRY(hipMalloc((void**)&h->d_n2, (nw + 8) * sizeof(u32)));
+        HIP_TRY(hipMalloc((void**)&h->d_n2, (nw + 8 + 4 * 512) * sizeof(u32)));  // N2, ctr, hist
         HIP_TRY(hipMemsetAsync(h->d_n2, 0, (nw + 8) * sizeof(u32), h->stream));
     }
     if (h->list_cap < n) {
@@ -508,11 +513,14 @@ static int signed_fold_bucketed(gcc_signed* h, const u64* edges, u64 n, const u3
     a.slow0 = h->d_lists + h->list_cap;
     a.slow1 = h->d_lists + 2 * h->list_cap;
     a.ctr = h->d_n2 + nw;
+    a.hist = h->d_n2 + nw + 8;
     a.levels = h->bucket_levels;
+    const char* stats = std::getenv("GELLY_BUCKET_STATS");
+    a.want_counts = stats && *stats && *stats != '0';
     int rc = gcc_internal_signed_bucket(h->bk_scratch, &a);
     if (rc) return rc;
     std::memcpy(h->last_counts, a.counts, sizeof(a.counts));
-    if (const char* e = std::getenv("GELLY_BUCKET_STATS"); e && *e && *e != '0')
+    if (a.want_counts)
         std::fprintf(stderr, "[signed-bucket] n=%llu level 1: emitted %llu slow %llu; level 2: emitted %llu slow %llu\n",
                      (unsigned long long)n, (unsigned long long)a.counts[0], (unsigned long long)a.counts[1],
                      (unsigned long long)a.counts[2], (unsigned long long)a.counts[3]);
@@ -536,7 +544,7 @@ static int signed_fold(gcc_signed* h, const u32* d_pairs, u64 n) {
     hipLaunchKernelGGL(signed_vote_kernel, dim3(1), dim3(1024), 0, h->stream, h->d_word, edges, s, vote);
     HIP_TRY(hipGetLastError());
     const u32 min_count = (u32)std::max(1.0, h->min_share * kVoteSamples);
-    hipLaunchKernelGGL(signed_snapshot_kernel, dim3(grid_for_n(nw, kMaxGrid)), dim3(256), 0, h->stream, h->d_word, h->cap,
+    hipLaunchKernelGGL(signed_snapshot_kernel, dim3(grid_for_n(nw * 16, kMaxGrid)), dim3(256), 0, h->stream, h->d_word, h->cap,
                        vote, min_count, h->d_gbits);
     HIP_TRY(hipGetLastError());
     if (n > s && h->bucket && n - s >= h->bucket_min && h->cap <= (1u << 28) &&

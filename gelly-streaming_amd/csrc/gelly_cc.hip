@@ -2885,7 +2885,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
         HIP_TRY(hipEventRecord(h->aux_ev[1], h->aux_stream));
     }
     rc = launch_k(h, "bucket_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, h->cap, h->d_meta,
-                  p1_blocks, p2_blocks, chunk);
+                  p1_blocks, p2_blocks, chunk, (const u32*)nullptr, (const u32*)nullptr);
     if (!rc)
         rc = ns > 256  // beyond 2^27 ids: 512 buckets' state and the 16K-edge tile exceed the LDS; 12K-edge tiles
                  ? launch_k(h, "bucket", n, bk::bucket_kernel<1024, 12, 512>, dim3(h->n_cu), dim3(1024),
@@ -3279,8 +3279,10 @@ static int counts(gcc_forest* h, unsigned long long out[2]) {
     return stream_sync_checked(h);
 }
 // P1 of the bucketed fold alone (layout + bucket_kernel), into f's bucket storage: n u64 pairs split by the FIRST id's
-// 2^19-id slice. For the signed forest's bucketed fold (signed_bucket.h), which treats P1 as a plain partition.
-static int bucketize(gcc_forest* f, const u64* edges, u64 n, u32** lo_out, bk::u16** hi_out) {
+// 2^19-id slice. For the signed forest's bucketed fold (signed_bucket.h), which treats P1 as a plain partition. n_dev:
+// the list's length on the device (n: its bound), exact: its per-slice counts (no sampled layout).
+static int bucketize(gcc_forest* f, const u64* edges, u64 n, u32** lo_out, bk::u16** hi_out, const u32* n_dev = nullptr,
+                     const u32* exact = nullptr) {
     const u32 ns = bucket_slices(f);
     if (!f->d_meta) HIP_TRY(hipMalloc((void**)&f->d_meta, sizeof(bk::Meta)));
     const u32 p1_blocks = 2 * (u32)f->n_cu;
@@ -3294,13 +3296,14 @@ static int bucketize(gcc_forest* f, const u64* edges, u64 n, u32** lo_out, bk::u
     bk::u16* bk_hi = reinterpret_cast<bk::u16*>(f->d_bk + 4 * bk_S);
     const u32 ovf_cap = (u32)std::min<u64>(f->ovf_cap, 0xFFFFFFF0ull);
     rc = launch_k(f, "sb_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, f->cap, f->d_meta,
-                  p1_blocks, p2_blocks, chunk);
+                  p1_blocks, p2_blocks, chunk, n_dev, exact);
+    const u64 nk = n_dev ? ~0ull : n;  // bucket_kernel: from the layout
     if (!rc)
         rc = ns > 256 ? launch_k(f, "sb_bucket", n, bk::bucket_kernel<1024, 12, 512>, dim3(f->n_cu), dim3(1024),
-                                 bk::p1_lds(1024, 12, 512), edges, n, ns, f->cap, f->d_meta, bk_lo, bk_hi, f->d_ovf,
+                                 bk::p1_lds(1024, 12, 512), edges, nk, ns, f->cap, f->d_meta, bk_lo, bk_hi, f->d_ovf,
                                  ovf_cap, f->d_err, (u32*)nullptr)
                       : launch_k(f, "sb_bucket", n, bk::bucket_kernel<1024, 16>, dim3(f->n_cu), dim3(1024),
-                                 bk::p1_lds(1024, 16), edges, n, ns, f->cap, f->d_meta, bk_lo, bk_hi, f->d_ovf, ovf_cap,
+                                 bk::p1_lds(1024, 16), edges, nk, ns, f->cap, f->d_meta, bk_lo, bk_hi, f->d_ovf, ovf_cap,
                                  f->d_err, (u32*)nullptr);
     *lo_out = bk_lo;
     *hi_out = bk_hi;
@@ -3308,7 +3311,9 @@ static int bucketize(gcc_forest* f, const u64* edges, u64 n, u32** lo_out, bk::u
 }
 
 // The bucketed signed fold (signed_bucket.h's header comment): `levels` rounds of P1 + filter + P1 + check + join, the
-// rest, the closing compress into a->out. Synchronises twice per level (the emitted and slow counts size the next P1).
+// rest, the closing compress into a->out. No host synchronisation: the lists' lengths and per-slice counts stay on
+// the device (ctr[1], ctr[2]; a->hist), and their P1 layouts take them from there (round 5: one sync per list and a
+// sampled layout each cost 0.3 ms of the share's 4.65).
 int gcc_internal_signed_bucket(gcc_forest* f, GccSignedBucketArgs* a) {
     DeviceGuard g(f->device);
     f->stream = a->stream;
@@ -3318,59 +3323,52 @@ int gcc_internal_signed_bucket(gcc_forest* f, GccSignedBucketArgs* a) {
     const u32 cps = std::max<u32>(1, (items + ns - 1) / ns);
     const size_t lds = sb::kSliceW * sizeof(u32);
     auto ovf_cap = [&]() -> u32 { return (u32)std::min<u64>(f->ovf_cap, 0xFFFFFFF0ull); };  // grows with the lists
+    const int levels = std::max(1, std::min(2, a->levels));
     int rc = GCC_OK;
-    const u64* src = a->edges;
-    u64 n = a->n;
     u64* slow_out = a->slow0;
     HIP_TRY(hipMemsetAsync(a->ctr, 0, 8 * sizeof(u32), f->stream));
-    for (int lv = 0; lv < std::max(1, std::min(2, a->levels)) && n >= 64 && !rc; ++lv) {
-        u32* lo;
-        bk::u16* hi;
-        rc = bucketize(f, src, n, &lo, &hi);
+    HIP_TRY(hipMemsetAsync(a->hist, 0, 2 * levels * bk::kMaxBuckets * sizeof(u32), f->stream));
+    const u64* src = a->edges;
+    u32* lo;
+    bk::u16* hi;
+    for (int lv = 0; lv < levels && !rc; ++lv) {
+        u32* he = a->hist + 2 * lv * bk::kMaxBuckets;
+        u32* hs = he + bk::kMaxBuckets;
+        // level 1: the batch (sampled layout); level 2: the previous level's slow list (its length ctr[2], its counts)
+        rc = lv == 0 ? bucketize(f, src, a->n, &lo, &hi)
+                     : bucketize(f, src, a->n, &lo, &hi, a->ctr + 2, he - bk::kMaxBuckets);
         if (!rc) HIP_TRY(hipMemsetAsync(a->ctr, 0, 3 * sizeof(u32), f->stream));
         if (!rc)
-            rc = launch_k(f, "sb_filter", n, sb::sb_filter_kernel, dim3(f->n_cu), dim3(sb::kBlock), lds, (const u32*)lo,
-                          (const bk::u16*)hi, (const bk::Meta*)f->d_meta, ns, cps, a->ctr, (const u32*)a->gbits, nw16,
-                          a->emit, slow_out, a->cap, f->d_err);
+            rc = launch_k(f, "sb_filter", lv == 0 ? a->n : 0, sb::sb_filter_kernel, dim3(f->n_cu), dim3(sb::kBlock), lds,
+                          (const u32*)lo, (const bk::u16*)hi, (const bk::Meta*)f->d_meta, ns, cps, a->ctr,
+                          (const u32*)a->gbits, nw16, a->emit, slow_out, a->cap, he, hs, f->d_err);
         // the bucketing's overflow list (edges): the rest's rule now (exact at any time: deferred members are never
         // united directly); a spill sets ctr[3] for the whole batch at the end
         if (!rc)
             rc = launch_k(f, "sb_rest", 0, sb::sb_rest_kernel, dim3(grid_for(std::max<u64>(1, ovf_cap()), 1024)), dim3(256), 0,
                           a->word, (const u64*)f->d_ovf, (u64)ovf_cap(), (const u32*)&f->d_meta->ovf_cur, 0u,
                           (const bk::Meta*)f->d_meta, a->gbits, a->vote, a->cap, a->fail, a->ctr);
-        if (rc) return rc;
-        u32 cnt[2];
-        HIP_TRY(hipMemcpyAsync(cnt, a->ctr + 1, sizeof(cnt), hipMemcpyDeviceToHost, f->stream));
-        rc = stream_sync_checked(f);
-        if (rc) return rc;
-        a->counts[2 * lv] = cnt[0];
-        a->counts[2 * lv + 1] = cnt[1];
-        if (cnt[0] >= 64) {  // the emitted pairs by v's slice, then checked / added with v's slice in LDS
-            rc = bucketize(f, a->emit, cnt[0], &lo, &hi);
-            if (!rc) HIP_TRY(hipMemsetAsync(a->ctr, 0, sizeof(u32), f->stream));
-            if (!rc)
-                rc = launch_k(f, "sb_check", cnt[0], sb::sb_check_kernel, dim3(f->n_cu), dim3(sb::kBlock), lds,
-                              (const u32*)lo, (const bk::u16*)hi, (const bk::Meta*)f->d_meta, ns, cps, a->ctr,
-                              (const u32*)a->gbits, nw16, a->n2, a->cap, a->fail, f->d_err);
-            if (!rc)
-                rc = launch_k(f, "sb_check_ovf", 0, sb::sb_check_list_kernel, dim3(grid_for(std::max<u64>(1, ovf_cap()), 1024)),
-                              dim3(256), 0, (const u64*)f->d_ovf, ovf_cap(), (const bk::Meta*)f->d_meta,
-                              (const u32*)a->gbits, a->n2, a->cap, a->fail, a->ctr);
-        } else if (cnt[0]) {  // a handful: against the global snapshot straight away
-            rc = launch_k(f, "sb_check_ovf", 0, sb::sb_check_list_kernel, dim3(1), dim3(256), 0, (const u64*)a->emit,
-                          (u32)cnt[0], (const bk::Meta*)nullptr, (const u32*)a->gbits, a->n2, a->cap, a->fail, a->ctr);
-        }
+        // the emitted pairs by v's slice (their length ctr[1]), then checked / added with v's slice in LDS
+        if (!rc) rc = bucketize(f, a->emit, a->n, &lo, &hi, a->ctr + 1, he);
+        if (!rc) HIP_TRY(hipMemsetAsync(a->ctr, 0, sizeof(u32), f->stream));
+        if (!rc)
+            rc = launch_k(f, "sb_check", 0, sb::sb_check_kernel, dim3(f->n_cu), dim3(sb::kBlock), lds, (const u32*)lo,
+                          (const bk::u16*)hi, (const bk::Meta*)f->d_meta, ns, cps, a->ctr, (const u32*)a->gbits, nw16,
+                          a->n2, a->cap, a->fail, f->d_err);
+        if (!rc)
+            rc = launch_k(f, "sb_check_ovf", 0, sb::sb_check_list_kernel, dim3(grid_for(std::max<u64>(1, ovf_cap()), 1024)),
+                          dim3(256), 0, (const u64*)f->d_ovf, ovf_cap(), (const bk::Meta*)f->d_meta,
+                          (const u32*)a->gbits, a->n2, a->cap, a->fail, a->ctr);
         if (!rc)
             rc = launch_k(f, "sb_join", 0, sb::sb_join_kernel, dim3(grid_for(nw16, kMaxGrid)), dim3(256), 0, a->word,
                           a->gbits, a->n2, nw16, a->vote, a->fail);
         src = slow_out;
-        n = cnt[1];
         slow_out = slow_out == a->slow0 ? a->slow1 : a->slow0;
     }
-    // the last level's slow edges, then (only after a spill: ctr[3]) the whole batch again
-    if (!rc && n)
-        rc = launch_k(f, "sb_rest", n, sb::sb_rest_kernel, dim3(grid_for(n, kMaxGrid)), dim3(256), 0, a->word, src, n,
-                      (const u32*)nullptr, 0u, (const bk::Meta*)nullptr, a->gbits, a->vote, a->cap, a->fail, a->ctr);
+    // the last level's slow edges (ctr[2] of them), then (only after a spill: ctr[3]) the whole batch again
+    if (!rc)
+        rc = launch_k(f, "sb_rest", 0, sb::sb_rest_kernel, dim3(grid_for(a->n, kMaxGrid)), dim3(256), 0, a->word, src, a->n,
+                      (const u32*)(a->ctr + 2), 0u, (const bk::Meta*)nullptr, a->gbits, a->vote, a->cap, a->fail, a->ctr);
     if (!rc)
         rc = launch_k(f, "sb_rest", 0, sb::sb_rest_kernel, dim3(grid_for(a->n, kMaxGrid)), dim3(256), 0, a->word,
                       a->edges, a->n, (const u32*)nullptr, 1u, (const bk::Meta*)nullptr, a->gbits, a->vote, a->cap,
@@ -3378,6 +3376,13 @@ int gcc_internal_signed_bucket(gcc_forest* f, GccSignedBucketArgs* a) {
     if (!rc)
         rc = launch_k(f, "sb_compress", 0, sb::sb_compress_kernel, dim3(grid_for(a->cap, kMaxGrid)), dim3(256), 0, a->word,
                       a->out, a->cap, (const u32*)a->gbits, a->vote);
+    if (!rc && a->want_counts) {  // diagnostics: the lists' lengths from the per-slice counts
+        std::vector<u32> h(2 * levels * bk::kMaxBuckets);
+        HIP_TRY(hipMemcpyAsync(h.data(), a->hist, h.size() * sizeof(u32), hipMemcpyDeviceToHost, f->stream));
+        rc = stream_sync_checked(f);
+        for (int i = 0; i < 4; ++i) a->counts[i] = 0;
+        for (size_t i = 0; i < h.size(); ++i) a->counts[i / bk::kMaxBuckets] += h[i];
+    }
     return rc;
 }
 

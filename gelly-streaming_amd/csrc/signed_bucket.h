@@ -98,11 +98,16 @@ __global__ __launch_bounds__(kBlock) void sb_filter_kernel(const u32* __restrict
                                                            const bk::Meta* __restrict__ m, u32 ns, u32 cps,
                                                            u32* __restrict__ ctr, const u32* __restrict__ gbits, u32 nw16,
                                                            u64* __restrict__ emit, u64* __restrict__ slow, u32 cap,
+                                                           u32* __restrict__ hist_e, u32* __restrict__ hist_s,
                                                            u32* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) u32 s_bits[];  // kSliceW
     __shared__ u32 s_item, s_wc[2 * (kBlock / 64)], s_base[2];
+    // the lists' entries per slice of their first id (the emitted target, the slow edge's other end): the next P1's
+    // exact layout (no sample; bucket_layout_kernel `exact`)
+    __shared__ u32 s_he[bk::kMaxBuckets], s_hs[bk::kMaxBuckets];
     const Appender ap{s_wc, s_base};
     typedef u32 u4 __attribute__((ext_vector_type(4)));
+    for (u32 s = threadIdx.x; s < ns; s += kBlock) s_he[s] = s_hs[s] = 0;
     const u32 n_items = ns * cps;
     u32 cur = 0xFFFFFFFFu;
     while (true) {
@@ -157,16 +162,23 @@ __global__ __launch_bounds__(kBlock) void sb_filter_kernel(const u32* __restrict
                         if (u != v) {
                             val[j] = (u64)v | ((u64)(((b >> 1) & 1u) ^ 1u) << 32);
                             em |= 1u << j;
+                            atomicAdd(&s_he[v >> kSliceBits], 1u);
                         }
                     } else {  // slow: listed with its ends SWAPPED, so that the next level looks at the other end
                         val[j] = ((u64)u << 32) | v;
                         smk |= 1u << j;
+                        atomicAdd(&s_hs[v >> kSliceBits], 1u);
                     }
                 }
             }
             if (bad) bk::flag_err(err, bk::kErrP2);
             append2<4 * kGroups>(ap, ctr + 1, emit, slow, em, smk, val);
         }
+    }
+    __syncthreads();
+    for (u32 s = threadIdx.x; s < ns; s += kBlock) {
+        if (s_he[s]) atomicAdd(&hist_e[s], s_he[s]);
+        if (s_hs[s]) atomicAdd(&hist_s[s], s_hs[s]);
     }
 }
 
