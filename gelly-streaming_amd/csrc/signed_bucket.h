@@ -41,10 +41,22 @@ constexpr int kGroups = 4;                         // 4-entry groups per lane pe
 
 __device__ __forceinline__ u32 pair2(u32 w, u32 x) { return (w >> (2 * (x & 15))) & 3u; }
 
-// the slice's 2-bit words of the snapshot into LDS (beyond the id range: zero)
+// the slice's 2-bit words of the snapshot into LDS (beyond the id range: zero). 16-B loads, all of a thread's in flight
+// before its LDS stores (a word per iteration waited out one load latency per word: 32 per thread per slice)
 __device__ __forceinline__ void load_slice2(u32* s, const u32* __restrict__ g, u32 sl, u32 nw16) {
+    typedef u32 u4 __attribute__((ext_vector_type(4)));
     const u32 w0 = sl * kSliceW;
-    for (u32 w = threadIdx.x; w < kSliceW; w += kBlock) s[w] = w0 + w < nw16 ? g[w0 + w] : 0u;
+    if (w0 + kSliceW <= nw16 && blockDim.x == kBlock) {  // a whole slice: 8 x 16 B per thread
+        constexpr int kPer = kSliceW / 4 / kBlock;
+        const u4* q = reinterpret_cast<const u4*>(g + w0);
+        u4 v[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) v[k] = q[k * kBlock + threadIdx.x];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) reinterpret_cast<u4*>(s)[k * kBlock + threadIdx.x] = v[k];
+        return;
+    }
+    for (u32 w = threadIdx.x; w < kSliceW; w += blockDim.x) s[w] = w0 + w < nw16 ? g[w0 + w] : 0u;
 }
 
 // Block-aggregated appends of this round's entries (K per lane: entry c goes to list 0 if bit c of m0 is set, to
@@ -187,12 +199,24 @@ __global__ __launch_bounds__(kBlock) void sb_filter_kernel(const u32* __restrict
 __device__ __forceinline__ void flush_slice2(const u32* s, const u32* __restrict__ gbits, u32* __restrict__ n2, u32 sl,
                                              u32 nw16) {
     const u32 w0 = sl * kSliceW;
-    for (u32 w = threadIdx.x; w < kSliceW && w0 + w < nw16; w += kBlock) {
-        const u32 lw = s[w];
-        const u32 nm = lw & ~gbits[w0 + w] & kMask2;  // members this block added
-        if (!nm) continue;
-        const u32 p1 = (lw >> 1) & nm;
-        atomicOr(&n2[w0 + w], (nm & ~p1) | (p1 << 1));
+    constexpr int kPer = 8;  // the snapshot's words of a batch of 8 LDS words in flight together
+    for (u32 wb = 0; wb < kSliceW; wb += kPer * kBlock) {
+        u32 g[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const u32 w = wb + k * kBlock + threadIdx.x;
+            g[k] = w < kSliceW && w0 + w < nw16 ? gbits[w0 + w] : ~0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const u32 w = wb + k * kBlock + threadIdx.x;
+            if (w >= kSliceW || w0 + w >= nw16) continue;
+            const u32 lw = s[w];
+            const u32 nm = lw & ~g[k] & kMask2;  // members this block added
+            if (!nm) continue;
+            const u32 p1 = (lw >> 1) & nm;
+            atomicOr(&n2[w0 + w], (nm & ~p1) | (p1 << 1));
+        }
     }
 }
 
