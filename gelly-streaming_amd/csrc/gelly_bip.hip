@@ -123,22 +123,33 @@ __global__ __launch_bounds__(256) void signed_snapshot_kernel(u32* __restrict__ 
     const u32 r = vote[0];
     const u32 nw = (n + 15) / 16;
     const u64 ids = (u64)nw * 16;
-    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i - threadIdx.x % 64 < ids; i += (u64)gridDim.x * 256) {
-        const u32 v = (u32)i;  // whole waves iterate together (the shuffles): ids past the range contribute nothing
-        u32 b = 0;
-        if (on && i < n) {
-            const u32 w = word[v];
-            if (w != kUnseen) {
+    const u64 stride = (u64)gridDim.x * 256;
+    const u32 lane = threadIdx.x % 64;
+    constexpr int kU = 4;  // ids per lane per iteration, their loads in flight together
+    for (u64 i0 = (u64)blockIdx.x * 256 + threadIdx.x; i0 - lane < ids; i0 += kU * stride) {
+        u32 wk[kU];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            const u64 i = i0 + k * stride;
+            wk[k] = on && i < n ? word[i] : kUnseen;
+        }
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            const u64 i = i0 + k * stride;
+            if (i - lane >= ids) break;  // whole waves (the shuffles): ids past the range contribute nothing
+            const u32 v = (u32)i;
+            u32 b = 0;
+            if (wk[k] != kUnseen) {
                 u32 par = 0;
-                const u32 root = sw_parent(w) == v ? v : sfind(word, v, w, par);
+                const u32 root = sw_parent(wk[k]) == v ? v : sfind(word, v, wk[k], par);
                 if (root == r) b = (1u | par << 1) << (2 * (v & 15));
             }
+            b |= __shfl_xor(b, 1, 64);
+            b |= __shfl_xor(b, 2, 64);
+            b |= __shfl_xor(b, 4, 64);
+            b |= __shfl_xor(b, 8, 64);
+            if ((v & 15) == 0 && i < ids) gbits[v >> 4] = b;
         }
-        b |= __shfl_xor(b, 1, 64);
-        b |= __shfl_xor(b, 2, 64);
-        b |= __shfl_xor(b, 4, 64);
-        b |= __shfl_xor(b, 8, 64);
-        if ((v & 15) == 0 && i < ids) gbits[v >> 4] = b;
     }
 }
 

@@ -309,8 +309,15 @@ __global__ __launch_bounds__(256) void sb_check_list_kernel(const u64* __restric
 __global__ __launch_bounds__(256) void sb_join_kernel(u32* __restrict__ word, u32* __restrict__ gbits, u32* __restrict__ n2,
                                                       u32 nw16, const u32* __restrict__ vote, u32* __restrict__ fail) {
     const u32 r = vote[0];
-    for (u32 w = blockIdx.x * 256 + threadIdx.x; w < nw16; w += gridDim.x * 256) {
-        const u32 h = n2[w];
+    const u32 stride = gridDim.x * 256;
+    constexpr int kU = 4;  // words per lane per iteration, their loads in flight together
+    for (u32 w0 = blockIdx.x * 256 + threadIdx.x; w0 < nw16; w0 += kU * stride) {
+      u32 hk[kU];
+#pragma unroll
+      for (int k = 0; k < kU; ++k) hk[k] = w0 + k * stride < nw16 ? n2[w0 + k * stride] : 0u;
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const u32 w = w0 + k * stride, h = hk[k];
         if (!h) continue;
         atomicExch(&n2[w], 0u);  // memory-side: the next level's ORs follow in later kernels
         const u32 h0 = h & kMask2, h1 = (h >> 1) & kMask2;
@@ -321,6 +328,7 @@ __global__ __launch_bounds__(256) void sb_join_kernel(u32* __restrict__ word, u3
             const u32 j = (u32)__builtin_ctz(d) >> 1, x = w * 16 + j;
             if (x < r || suf::ld(&word[x]) != suf::kUnseen) suf::unite(word, x, r, (h1 >> (2 * j)) & 1u, fail);
         }
+      }
     }
 }
 
@@ -373,21 +381,32 @@ __global__ __launch_bounds__(256) void sb_compress_kernel(u32* __restrict__ word
     __syncthreads();
     const u32 rf = s_rf, pr = s_pr;
     const u64 stride = (u64)gridDim.x * 256;
-    for (u64 i = (u64)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-        const u32 v = (u32)i;
-        const u32 b = pair2(gbits[v >> 4], v);
-        if (b & 1u) {
-            out[v] = (rf << 1) | (((b >> 1) & 1u) ^ pr);
-            continue;
+    constexpr int kU = 4;  // ids per lane per iteration, their loads in flight together
+    for (u64 i0 = (u64)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += kU * stride) {
+        u32 bw[kU], ww[kU];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            const u64 i = i0 + k * stride;
+            bw[k] = i < n ? gbits[i >> 4] : 0u;
+            ww[k] = i < n ? word[i] : suf::kUnseen;
         }
-        const u32 w = word[v];
-        if (w == suf::kUnseen || suf::parent_of(w) == v) {
-            out[v] = w;
-            continue;
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            const u64 i = i0 + k * stride;
+            if (i >= n) break;
+            const u32 v = (u32)i;
+            const u32 b = pair2(bw[k], v);
+            const u32 w = ww[k];
+            if (b & 1u) {
+                out[v] = (rf << 1) | (((b >> 1) & 1u) ^ pr);
+            } else if (w == suf::kUnseen || suf::parent_of(w) == v) {
+                out[v] = w;
+            } else {
+                u32 par;
+                const u32 root = suf::find_ro(word, v, w, par);
+                out[v] = (root << 1) | par;
+            }
         }
-        u32 par;
-        const u32 root = suf::find_ro(word, v, w, par);
-        out[v] = (root << 1) | par;
     }
 }
 
