@@ -468,6 +468,7 @@ struct gcc_signed {
     int bucket = 1;
     u64 bucket_min = 1ull << 22;
     int bucket_levels = 2;
+    int bucket_items = 2;              // "bucket_items": work items (slice parts) per CU of its filter / check kernels (a slice load each: 2 beat 1, 4, 8, 16 — profiles/r5ao_sweep_bip_items.txt)
     gcc_forest* bk_scratch = nullptr;  // a CC forest of the same id range: its bucket storage (P1) only
     u32* d_n2 = nullptr;               // 2 bits per id + the 8 counter words behind them
     u64* d_lists = nullptr;            // the emit list and two slow lists
@@ -526,6 +527,7 @@ static int signed_fold_bucketed(gcc_signed* h, const u64* edges, u64 n, const u3
     a.ctr = h->d_n2 + nw;
     a.hist = h->d_n2 + nw + 8;
     a.levels = h->bucket_levels;
+    a.items_per_cu = h->bucket_items;
     const char* stats = std::getenv("GELLY_BUCKET_STATS");
     a.want_counts = stats && *stats && *stats != '0';
     int rc = gcc_internal_signed_bucket(h->bk_scratch, &a);
@@ -777,6 +779,9 @@ int gcc_signed_tune(gcc_signed* h, const char* key, double value) {
     } else if (k == "bucket_min") {
         CHECK_ARG(value >= 0, "bucket_min must be >= 0");
         h->bucket_min = (u64)value;
+    } else if (k == "bucket_items") {
+        CHECK_ARG(value >= 1 && value <= 64, "bucket_items must be in [1, 64]");
+        h->bucket_items = (int)value;
     } else if (k == "bucket_levels") {
         CHECK_ARG(value == 1 || value == 2, "bucket_levels must be 1 or 2");
         h->bucket_levels = (int)value;

@@ -3319,7 +3319,7 @@ int gcc_internal_signed_bucket(gcc_forest* f, GccSignedBucketArgs* a) {
     f->stream = a->stream;
     const u32 ns = bucket_slices(f);
     const u32 nw16 = (u32)(((u64)a->cap + 15) / 16);
-    const u32 items = 4 * (u32)f->n_cu;
+    const u32 items = (u32)std::max(1, a->items_per_cu) * (u32)f->n_cu;
     const u32 cps = std::max<u32>(1, (items + ns - 1) / ns);
     const size_t lds = sb::kSliceW * sizeof(u32);
     auto ovf_cap = [&]() -> u32 { return (u32)std::min<u64>(f->ovf_cap, 0xFFFFFFF0ull); };  // grows with the lists

@@ -24,6 +24,7 @@ struct GccSignedBucketArgs {
     uint32_t* ctr;          // scratch: 8 device words
     uint32_t* hist;         // scratch: 4 x 512 device words (per level, the emit and slow lists' per-slice counts)
     int levels;             // filter levels (1 or 2) before the rest
+    int items_per_cu;       // work items (slice parts) of the filter and check kernels per CU
     int want_counts;        // 1: fill counts (synchronises)
     uint64_t counts[4];     // out: emitted and slow entries of level 1, of level 2 (diagnostics)
 };

@@ -244,7 +244,8 @@ def test_giant_fold_knobs_and_no_dominant_component():
         for knobs in ({}, {"sample_shift": 1}, {"sample_shift": 10}, {"min_share": 1.0}, {"min_share": 0.001},
                       {"unroll": 1}, {"unroll": 8}, {"xcd": 1, "xcd_min": 0}, {"xcd": 1, "xcd_min": 0, "min_share": 1.0},
                       {"xcd": 1, "xcd_min": 0, "sample_shift": 10}, {"xcd": 1}, {"bucket": 0}, {"bucket_levels": 1},
-                      {"bucket_min": 0, "sample_shift": 10}, {"min_share": 0.001, "bucket_levels": 1}):
+                      {"bucket_min": 0, "sample_shift": 10}, {"min_share": 0.001, "bucket_levels": 1},
+                      {"bucket_items": 1}, {"bucket_items": 16}):
             c = Candidates(V).tune(**knobs)
             c.fold_device(d.data_ptr(), E)
             assert c.getSuccess() and np.array_equal(c.words(), want), (cfg.name, knobs)
