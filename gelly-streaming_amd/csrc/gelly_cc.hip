@@ -2033,7 +2033,8 @@ struct FoldTune {
     // the bucketed fold also for a later window of a forest tracking a giant (C4 in 8 windows: every window after the
     // first took the filtered fold over an 8 MiB global bitmap, 2.2 ms per 2^27 edges; round 4)
     int bucket_windows = 1;
-    int bucket_items = 4;  // P2 / P3 work items per CU (each loads its slice's bitmap into LDS)
+    int bucket_items = 4;  // P2 work items per CU (each loads its slice's bitmap into LDS)
+    int bucket_items_p3 = 2;  // FINAL / second-level P3 work items per CU
     // tests only: the fail_absorb-th next gcc_forest_absorb_many call fails with GCC_E_INTERNAL before it launches
     // anything (0: never) — a rank's absorb failing inside the cross-GPU group merge (tests/test_gpu_group.py)
     int fail_absorb = 0;
@@ -2866,7 +2867,10 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     // bytes of slices, so a v-list has (slice size ratio) times fewer parts
     const u32 nvs = bk::vslices(h->cap);
     const u32 vratio = 1u << (bk::kVSliceBits - bk::kSliceBits);
-    const u32 cps_v = std::max<u32>(1, cps * ns / nvs / vratio);
+    // (round 5: P3's own count, bucket_items_p3 = 2 per CU: half P2's — fewer 128 KiB slice loads; C4 9.17 -> 9.1 ms,
+    // the share 1.82 -> 1.78 with both at 2, P2 itself slower at 2: profiles/r5aq_sweep_cc_items.txt)
+    const u32 cps3 = std::max<u32>(1, ((u32)std::max(1, t.bucket_items_p3) * (u32)h->n_cu + ns - 1) / ns);
+    const u32 cps_v = std::max<u32>(1, cps3 * ns / nvs / vratio);
     const u32 cps_seed_v = std::max<u32>(1, cps_seed * ns / nvs / vratio);
     u32 slot = 0;
     // a fresh forest with the deferred N: C is deferred too (round 5), and P1 performs the lazy reset itself
@@ -4343,6 +4347,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "bucket_chunk") t.bucket_chunk = std::max(0, std::min((int)bk::kMaxChunk, (int)value));
     else if (k == "bucket_windows") t.bucket_windows = value != 0;
     else if (k == "bucket_items") t.bucket_items = std::max(1, std::min(64, (int)value));
+    else if (k == "bucket_items_p3") t.bucket_items_p3 = std::max(1, std::min(64, (int)value));
     else if (k == "bucket_slow2") t.bucket_slow2 = value != 0.0;
     else if (k == "bucket_defer") t.bucket_defer = value != 0.0;
     else if (k == "bucket_defer_c") t.bucket_defer_c = std::max(0, std::min(2, (int)value));

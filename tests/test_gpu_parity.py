@@ -567,6 +567,8 @@ KNOB_CASES = {
     "bucket_chunk": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_chunk": 64},
                      {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_chunk": 4096}],
     "bucket_items": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_items": 1},
+    "bucket_items_p3": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_items_p3": 1},
+                        {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_items_p3": 8}],
     # the later windows of this stream are short (4096 edges): bucket_min_batch 4096 lets them take the bucketed fold
     "bucket_windows": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 12, "bucket_windows": 0},
                        {"bucket_min_ids": 0, "bucket_min_batch": 1 << 12, "bucket_windows": 1}],
