@@ -193,6 +193,49 @@ def test_kron_hubs_vs_oracle(odd, giant, xcd, bucket):
     c.close()
 
 
+@pytest.mark.parametrize("spill", [False, True])
+def test_bucketed_fold_overflow_and_spill(spill):
+    """The bucketed signed fold's first bucketing takes its capacities from a sampled layout (64 runs of 1024 edges
+    spread over the batch past the fold's sample). A batch built against that layout: the sampled runs have their
+    sources in slice 0, the other edges (all of them, or 1/8) in slice 1, so bucket 1 is under-estimated. 1/8: the
+    excess goes to the overflow list (the rest's rule, at level 1); all: the overflow list overflows too (spill) and
+    the whole batch is folded again by the rest kernel. Both give the unbucketed fold's words; with an odd edge the
+    summary fails either way."""
+    import torch
+
+    V = 1 << 20
+    n = 1 << 22
+    s = max(1 << 20, n >> 6)  # gelly_bip.hip signed_fold: the sample (sample_shift 6)
+    rest = n - s
+    stride = rest // 64  # bucket_layout_kernel: run k = [k * stride, k * stride + 1024) of the rest
+    rng = np.random.default_rng(11 + spill)
+    # the sample: a star of 64 even hubs over odd ids (a dominant component for the vote), sources in slice 0
+    su = 2 * rng.integers(0, 64, size=s, dtype=np.uint32)
+    sv = 2 * rng.integers(0, V // 2, size=s, dtype=np.uint32) + 1
+    # the rest: even sources in slice 1 (all, or every 8th), slice 0 at the sampled runs; odd targets anywhere
+    ru = 2 * rng.integers(0, (1 << 19) // 2, size=rest, dtype=np.uint32)
+    hot = np.ones(rest, bool) if spill else (np.arange(rest) % 8 == 5)
+    ru[hot] += 1 << 19
+    sampled = (np.arange(rest) % stride) < 1024
+    ru[sampled] = 2 * rng.integers(0, (1 << 19) // 2, size=int(sampled.sum()), dtype=np.uint32)
+    rv = 2 * rng.integers(0, V // 2, size=rest, dtype=np.uint32) + 1
+    pairs = np.concatenate([np.stack([su, sv], axis=1), np.stack([ru, rv], axis=1)]).astype(np.uint32)
+    for odd in (False, True):
+        p = pairs.copy()
+        if odd:
+            p[s + rest // 2] = [p[0, 0], p[s + 1, 0]]  # two even ids: an even-even edge inside the giant
+        d = torch.from_numpy(p.reshape(-1).view(np.int32)).cuda()
+        ref = Candidates(V).tune(bucket=0)
+        ref.fold_device(d.data_ptr(), n)
+        c = Candidates(V).tune(bucket_min=0)
+        c.fold_device(d.data_ptr(), n)
+        assert c.getSuccess() == ref.getSuccess() == (not odd)
+        if not odd:
+            assert np.array_equal(c.words(), ref.words())
+        ref.close()
+        c.close()
+
+
 @pytest.mark.parametrize("odd", [False, True])
 @pytest.mark.parametrize("knobs", [{}, {"bucket_levels": 1}, {"sample_shift": 12}])
 def test_bucketed_fold_many_slices(odd, knobs):
