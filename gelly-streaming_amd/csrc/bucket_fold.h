@@ -379,7 +379,9 @@ constexpr size_t p1_lds(int block, int per, u32 maxb = 256, u32 w = 4) {
     return ((size_t)block * per + (w - 1) * maxb) * sizeof(u64);
 }
 
-template <int P1B, int P1P, u32 MAXB = 256, u32 W = 4>
+// KEYONLY (the signed fold's emit lists, signed_bucket.h): the second id is a parity bit, so an entry is 4 B — the
+// key's slice-local bits | second << kSliceBits in lo, no hi array (padding: lo = ~0)
+template <int P1B, int P1P, u32 MAXB = 256, u32 W = 4, bool KEYONLY = false>
 __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const u64* __restrict__ edges, u64 n, u32 ns, u32 cap,
                                                           Meta* __restrict__ m, u32* __restrict__ bk_lo,
                                                           u16* __restrict__ bk_hi, u64* __restrict__ ovf, u32 ovf_cap,
@@ -498,7 +500,16 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
             }
             const u32 s = (u32)e[0] >> kSliceBits;
             const u32 off = run_pos(runs, s, W * xw - s_start[s]);  // a multiple of W: all W in one chunk
-            if (off != 0xFFFFFFFFu) {
+            if (KEYONLY && off != 0xFFFFFFFFu) {
+                auto key_of = [](u64 x) -> u32 {
+                    return x == ~0ull ? 0xFFFFFFFFu : ((u32)x & (kSliceIds - 1)) | ((u32)(x >> 32) << kSliceBits);
+                };
+#pragma unroll
+                for (u32 k = 0; k < W / 4; ++k) {
+                    const u4 lo = {key_of(e[4 * k]), key_of(e[4 * k + 1]), key_of(e[4 * k + 2]), key_of(e[4 * k + 3])};
+                    *reinterpret_cast<u4*>(bk_lo + s_base[s] + off + 4 * k) = lo;
+                }
+            } else if (off != 0xFFFFFFFFu) {
 #pragma unroll
                 for (u32 k = 0; k < W / 4; ++k) {  // 16-B aligned (bases: 16-entry multiples)
                     const u4 lo = {bk_lo_of(e[4 * k]), bk_lo_of(e[4 * k + 1]), bk_lo_of(e[4 * k + 2]), bk_lo_of(e[4 * k + 3])};
@@ -529,7 +540,10 @@ __global__ __launch_bounds__(P1B, (P1B == 512 ? 4 : 4)) void bucket_kernel(const
     GCC_PH_FLUSH(phc, 0);
     // the unused tails of this block's chunks: padding entries (P2 skips them)
     for (u32 s = 0; s < ns; ++s)
-        for (u32 i = s_cpos[s] + threadIdx.x; i < s_cend[s]; i += P1B) bk_hi[s_base[s] + i] = kPadHi;
+        for (u32 i = s_cpos[s] + threadIdx.x; i < s_cend[s]; i += P1B) {
+            if (KEYONLY) bk_lo[s_base[s] + i] = 0xFFFFFFFFu;
+            else bk_hi[s_base[s] + i] = kPadHi;
+        }
     GCC_BT(0, 1);
 }
 

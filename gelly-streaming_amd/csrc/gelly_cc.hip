@@ -3286,7 +3286,7 @@ static int counts(gcc_forest* h, unsigned long long out[2]) {
 // 2^19-id slice. For the signed forest's bucketed fold (signed_bucket.h), which treats P1 as a plain partition. n_dev:
 // the list's length on the device (n: its bound), exact: its per-slice counts (no sampled layout).
 static int bucketize(gcc_forest* f, const u64* edges, u64 n, u32** lo_out, bk::u16** hi_out, const u32* n_dev = nullptr,
-                     const u32* exact = nullptr) {
+                     const u32* exact = nullptr, bool key_only = false) {
     const u32 ns = bucket_slices(f);
     if (!f->d_meta) HIP_TRY(hipMalloc((void**)&f->d_meta, sizeof(bk::Meta)));
     const u32 p1_blocks = 2 * (u32)f->n_cu;
@@ -3302,7 +3302,11 @@ static int bucketize(gcc_forest* f, const u64* edges, u64 n, u32** lo_out, bk::u
     rc = launch_k(f, "sb_layout", 0, bk::bucket_layout_kernel, dim3(1), dim3(1024), 0, edges, n, ns, f->cap, f->d_meta,
                   p1_blocks, p2_blocks, chunk, n_dev, exact);
     const u64 nk = n_dev ? ~0ull : n;  // bucket_kernel: from the layout
-    if (!rc)
+    if (!rc && key_only && ns <= 256)  // 4-B entries (the emit lists: the second id is a parity bit)
+        rc = launch_k(f, "sb_bucket", n, bk::bucket_kernel<1024, 16, 256, 4, true>, dim3(f->n_cu), dim3(1024),
+                      bk::p1_lds(1024, 16), edges, nk, ns, f->cap, f->d_meta, bk_lo, bk_hi, f->d_ovf, ovf_cap, f->d_err,
+                      (u32*)nullptr);
+    else if (!rc)
         rc = ns > 256 ? launch_k(f, "sb_bucket", n, bk::bucket_kernel<1024, 12, 512>, dim3(f->n_cu), dim3(1024),
                                  bk::p1_lds(1024, 12, 512), edges, nk, ns, f->cap, f->d_meta, bk_lo, bk_hi, f->d_ovf,
                                  ovf_cap, f->d_err, (u32*)nullptr)
@@ -3353,10 +3357,12 @@ int gcc_internal_signed_bucket(gcc_forest* f, GccSignedBucketArgs* a) {
                           a->word, (const u64*)f->d_ovf, (u64)ovf_cap(), (const u32*)&f->d_meta->ovf_cur, 0u,
                           (const bk::Meta*)f->d_meta, a->gbits, a->vote, a->cap, a->fail, a->ctr);
         // the emitted pairs by v's slice (their length ctr[1]), then checked / added with v's slice in LDS
-        if (!rc) rc = bucketize(f, a->emit, a->n, &lo, &hi, a->ctr + 1, he);
+        const bool key_only = ns <= 256;
+        if (!rc) rc = bucketize(f, a->emit, a->n, &lo, &hi, a->ctr + 1, he, key_only);
         if (!rc) HIP_TRY(hipMemsetAsync(a->ctr, 0, sizeof(u32), f->stream));
         if (!rc)
-            rc = launch_k(f, "sb_check", 0, sb::sb_check_kernel, dim3(f->n_cu), dim3(sb::kBlock), lds, (const u32*)lo,
+            rc = launch_k(f, "sb_check", 0, key_only ? sb::sb_check_kernel<true> : sb::sb_check_kernel<false>, dim3(f->n_cu),
+                          dim3(sb::kBlock), lds, (const u32*)lo,
                           (const bk::u16*)hi, (const bk::Meta*)f->d_meta, ns, cps, a->ctr, (const u32*)a->gbits, nw16,
                           a->n2, a->cap, a->fail, f->d_err);
         if (!rc)
@@ -3517,7 +3523,8 @@ static int set_lds_attrs_impl() {
         {(const void*)compress_inc_kernel<true, true>, (int)(gcc::kBloomBits / 8)},
         {(const void*)compress_pipe_kernel, (int)(gcc::kBloomBits / 8)},
         {(const void*)sb::sb_filter_kernel, (int)(sb::kSliceW * sizeof(u32))},
-        {(const void*)sb::sb_check_kernel, (int)(sb::kSliceW * sizeof(u32))},
+        {(const void*)sb::sb_check_kernel<true>, (int)(sb::kSliceW * sizeof(u32))},
+        {(const void*)sb::sb_check_kernel<false>, (int)(sb::kSliceW * sizeof(u32))},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, false>, filtered},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 8, true, false>, filtered},
         {(const void*)fold_filtered_kernel<true, kFilterBlockLds, 4, true, true>, filtered},
@@ -3537,6 +3544,7 @@ static int set_lds_attrs_impl() {
         {(const void*)bk::bucket_hub_kernel, (int)(2 * kHubSlots * sizeof(u32))},
         {(const void*)bk::bucket_kernel<512, 16>, (int)bk::p1_lds(512, 16)},
         {(const void*)bk::bucket_kernel<1024, 16>, (int)bk::p1_lds(1024, 16)},
+        {(const void*)bk::bucket_kernel<1024, 16, 256, 4, true>, (int)bk::p1_lds(1024, 16)},
         {(const void*)bk::bucket_kernel<1024, 12>, (int)bk::p1_lds(1024, 12)},
         {(const void*)bk::bucket_kernel<1024, 12, 512>, (int)bk::p1_lds(1024, 12, 512)},
         {(const void*)bk::bucket_kernel<1024, 16, 256, 8>, (int)bk::p1_lds(1024, 16, 256, 8)},

@@ -221,6 +221,7 @@ __device__ __forceinline__ void flush_slice2(const u32* s, const u32* __restrict
 }
 
 // Work items over the emit list's buckets (entries: v, parity p): see the header comment. ctr[0]: the item counter.
+template <bool KEYONLY>
 __global__ __launch_bounds__(kBlock) void sb_check_kernel(const u32* __restrict__ bk_lo, const bk::u16* __restrict__ bk_hi,
                                                           const bk::Meta* __restrict__ m, u32 ns, u32 cps,
                                                           u32* __restrict__ ctr, const u32* __restrict__ gbits, u32 nw16,
@@ -255,13 +256,19 @@ __global__ __launch_bounds__(kBlock) void sb_check_kernel(const u32* __restrict_
         const u64 g0 = lo / 4, g1 = (hi + 3) / 4;
         for (u64 g = g0 + threadIdx.x; g < g1; g += kBlock) {
             const u4 l4 = *reinterpret_cast<const u4*>(bk_lo + base + 4 * g);
-            const u64 h4 = *reinterpret_cast<const u64*>(bk_hi + base + 4 * g);
+            const u64 h4 = KEYONLY ? 0ull : *reinterpret_cast<const u64*>(bk_hi + base + 4 * g);
             const u32 lv[4] = {l4.x, l4.y, l4.z, l4.w};
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 u32 x, p;
                 const u64 e = 4 * g + c;
-                if (!bk::bk_decode(lv[c], (bk::u16)(h4 >> (16 * c)), sbase, x, p) || e < lo || e >= hi) continue;
+                if (KEYONLY) {  // 4-B entries: x's slice-local bits | p << kSliceBits (bucket_fold.h KEYONLY); ~0 = padding
+                    if (lv[c] == 0xFFFFFFFFu || e < lo || e >= hi) continue;
+                    x = sbase | (lv[c] & (bk::kSliceIds - 1));
+                    p = lv[c] >> kSliceBits;
+                } else if (!bk::bk_decode(lv[c], (bk::u16)(h4 >> (16 * c)), sbase, x, p) || e < lo || e >= hi) {
+                    continue;
+                }
                 if (x >= cap || p > 1u) {
                     bk::flag_err(err, bk::kErrP2);
                     continue;
