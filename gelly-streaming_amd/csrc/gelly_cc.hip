@@ -3370,6 +3370,9 @@ int gcc_internal_signed_bucket(gcc_forest* f, GccSignedBucketArgs* a) {
                           dim3(256), 0, (const u64*)f->d_ovf, ovf_cap(), (const bk::Meta*)f->d_meta,
                           (const u32*)a->gbits, a->n2, a->cap, a->fail, a->ctr);
         if (!rc)
+            rc = launch_k(f, "sb_join_low", 0, sb::sb_join_low_kernel, dim3(64), dim3(256), 0, a->word, (const u32*)a->n2,
+                          a->vote, a->fail);
+        if (!rc)
             rc = launch_k(f, "sb_join", 0, sb::sb_join_kernel, dim3(grid_for(nw16, kMaxGrid)), dim3(256), 0, a->word,
                           a->gbits, a->n2, nw16, a->vote, a->fail);
         src = slow_out;

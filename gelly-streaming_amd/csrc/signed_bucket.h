@@ -312,10 +312,36 @@ __global__ __launch_bounds__(256) void sb_check_list_kernel(const u64* __restric
     }
 }
 
+// The new members below r first (sb_join_low_kernel: the words below r's; each hooks C's root under a smaller id), so
+// that sb_join_kernel's unites of seen members start at a stable root: C's root R = root(r) found once per block, each
+// seen member united with R (parity composed with r's to R). Round 5: every unite walked from r, and the below-r hooks
+// made that walk a chain of successively smaller roots — the seen members' 706K unites cost the share's two joins
+// ~0.24 ms (a timing build without them: 73 against 195 us per join).
+__global__ __launch_bounds__(256) void sb_join_low_kernel(u32* __restrict__ word, const u32* __restrict__ n2,
+                                                          const u32* __restrict__ vote, u32* __restrict__ fail) {
+    const u32 r = vote[0];
+    for (u32 w = blockIdx.x * 256 + threadIdx.x; 16ull * w < r; w += gridDim.x * 256) {
+        const u32 h = n2[w];
+        const u32 h1 = (h >> 1) & kMask2;
+        for (u32 d = (h | h1) & kMask2; d; d &= d - 1) {
+            const u32 j = (u32)__builtin_ctz(d) >> 1, x = w * 16 + j;
+            if (x < r) suf::unite(word, x, r, (h1 >> (2 * j)) & 1u, fail);
+        }
+    }
+}
+
 // C |= N2 (see the header comment). r = vote[0], C's root at the snapshot. N2 is cleared for the next level.
 __global__ __launch_bounds__(256) void sb_join_kernel(u32* __restrict__ word, u32* __restrict__ gbits, u32* __restrict__ n2,
                                                       u32 nw16, const u32* __restrict__ vote, u32* __restrict__ fail) {
+    __shared__ u32 s_R, s_pr;
     const u32 r = vote[0];
+    if (threadIdx.x == 0) {
+        u32 pr = 0;
+        s_R = suf::find_ro(word, r, suf::ld(&word[r]), pr);
+        s_pr = pr;
+    }
+    __syncthreads();
+    const u32 R = s_R, pr = s_pr;  // a unite with R is exact whatever R has become meanwhile (the unite finds)
     const u32 stride = gridDim.x * 256;
     constexpr int kU = 4;  // words per lane per iteration, their loads in flight together
     for (u32 w0 = blockIdx.x * 256 + threadIdx.x; w0 < nw16; w0 += kU * stride) {
@@ -333,7 +359,8 @@ __global__ __launch_bounds__(256) void sb_join_kernel(u32* __restrict__ word, u3
         atomicOr(&gbits[w], nm | (h1 << 1));
         for (u32 d = nm; d; d &= d - 1) {
             const u32 j = (u32)__builtin_ctz(d) >> 1, x = w * 16 + j;
-            if (x < r || suf::ld(&word[x]) != suf::kUnseen) suf::unite(word, x, r, (h1 >> (2 * j)) & 1u, fail);
+            if (x >= r && suf::ld(&word[x]) != suf::kUnseen)  // (below r: sb_join_low_kernel)
+                suf::unite(word, x, R, ((h1 >> (2 * j)) & 1u) ^ pr, fail);
         }
       }
     }
