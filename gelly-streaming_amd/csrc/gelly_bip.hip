@@ -473,7 +473,7 @@ struct gcc_signed {
     u32* d_n2 = nullptr;               // 2 bits per id + the 8 counter words behind them
     u64* d_lists = nullptr;            // the emit list and two slow lists
     u64 list_cap = 0;                  // entries per list
-    u64 last_counts[4] = {0, 0, 0, 0}; // the last bucketed fold's emitted / slow entries per level (diagnostics)
+    u64 last_counts[6] = {0, 0, 0, 0, 0, 0};  // the last bucketed fold's emitted / slow entries per level (diagnostics)
     std::vector<u32> host_words;
     bool host_valid = false;
 };
@@ -497,7 +497,7 @@ static int signed_fold_bucketed(gcc_signed* h, const u64* edges, u64 n, const u3
     if (!h->bk_scratch) {
         int rc = gcc_forest_create(h->device, h->cap, &h->bk_scratch);
         if (rc) return rc;
-        HIP_TRY(hipMalloc((void**)&h->d_n2, (nw + 8 + 4 * 512) * sizeof(u32)));  // N2, ctr, hist
+        HIP_TRY(hipMalloc((void**)&h->d_n2, (nw + 8 + 6 * 512) * sizeof(u32)));  // N2, ctr, hist (2 per level)
         HIP_TRY(hipMemsetAsync(h->d_n2, 0, (nw + 8) * sizeof(u32), h->stream));
     }
     if (h->list_cap < n) {
@@ -534,9 +534,10 @@ static int signed_fold_bucketed(gcc_signed* h, const u64* edges, u64 n, const u3
     if (rc) return rc;
     std::memcpy(h->last_counts, a.counts, sizeof(a.counts));
     if (a.want_counts)
-        std::fprintf(stderr, "[signed-bucket] n=%llu level 1: emitted %llu slow %llu; level 2: emitted %llu slow %llu\n",
+        std::fprintf(stderr, "[signed-bucket] n=%llu level 1: emitted %llu slow %llu; level 2: emitted %llu slow %llu; level 3: emitted %llu slow %llu\n",
                      (unsigned long long)n, (unsigned long long)a.counts[0], (unsigned long long)a.counts[1],
-                     (unsigned long long)a.counts[2], (unsigned long long)a.counts[3]);
+                     (unsigned long long)a.counts[2], (unsigned long long)a.counts[3], (unsigned long long)a.counts[4],
+                     (unsigned long long)a.counts[5]);
     std::swap(h->d_word, h->d_spare);  // the closing compress wrote the canonical words
     h->compressed = true;
     h->host_valid = false;
@@ -783,7 +784,7 @@ int gcc_signed_tune(gcc_signed* h, const char* key, double value) {
         CHECK_ARG(value >= 1 && value <= 64, "bucket_items must be in [1, 64]");
         h->bucket_items = (int)value;
     } else if (k == "bucket_levels") {
-        CHECK_ARG(value == 1 || value == 2, "bucket_levels must be 1 or 2");
+        CHECK_ARG(value >= 1 && value <= 3, "bucket_levels must be 1, 2 or 3");
         h->bucket_levels = (int)value;
     } else if (k == "min_share") {
         CHECK_ARG(value > 0 && value <= 1, "min_share must be in (0, 1]");

@@ -3331,7 +3331,7 @@ int gcc_internal_signed_bucket(gcc_forest* f, GccSignedBucketArgs* a) {
     const u32 cps = std::max<u32>(1, (items + ns - 1) / ns);
     const size_t lds = sb::kSliceW * sizeof(u32);
     auto ovf_cap = [&]() -> u32 { return (u32)std::min<u64>(f->ovf_cap, 0xFFFFFFF0ull); };  // grows with the lists
-    const int levels = std::max(1, std::min(2, a->levels));
+    const int levels = std::max(1, std::min(3, a->levels));
     int rc = GCC_OK;
     u64* slow_out = a->slow0;
     HIP_TRY(hipMemsetAsync(a->ctr, 0, 8 * sizeof(u32), f->stream));
@@ -3393,7 +3393,7 @@ int gcc_internal_signed_bucket(gcc_forest* f, GccSignedBucketArgs* a) {
         std::vector<u32> h(2 * levels * bk::kMaxBuckets);
         HIP_TRY(hipMemcpyAsync(h.data(), a->hist, h.size() * sizeof(u32), hipMemcpyDeviceToHost, f->stream));
         rc = stream_sync_checked(f);
-        for (int i = 0; i < 4; ++i) a->counts[i] = 0;
+        for (int i = 0; i < 6; ++i) a->counts[i] = 0;
         for (size_t i = 0; i < h.size(); ++i) a->counts[i / bk::kMaxBuckets] += h[i];
     }
     return rc;

@@ -22,11 +22,11 @@ struct GccSignedBucketArgs {
     uint64_t* slow0;
     uint64_t* slow1;
     uint32_t* ctr;          // scratch: 8 device words
-    uint32_t* hist;         // scratch: 4 x 512 device words (per level, the emit and slow lists' per-slice counts)
-    int levels;             // filter levels (1 or 2) before the rest
+    uint32_t* hist;         // scratch: 6 x 512 device words (per level, the emit and slow lists' per-slice counts)
+    int levels;             // filter levels (1 to 3) before the rest
     int items_per_cu;       // work items (slice parts) of the filter and check kernels per CU
     int want_counts;        // 1: fill counts (synchronises)
-    uint64_t counts[4];     // out: emitted and slow entries of level 1, of level 2 (diagnostics)
+    uint64_t counts[6];     // out: emitted and slow entries of levels 1-3 (diagnostics)
 };
 
 // gcc status; `scratch` = a CC forest of the same id range, used for its bucket storage only (gcc_forest_create)

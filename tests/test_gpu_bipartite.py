@@ -237,7 +237,8 @@ def test_bucketed_fold_overflow_and_spill(spill):
 
 
 @pytest.mark.parametrize("odd", [False, True])
-@pytest.mark.parametrize("knobs", [{}, {"bucket_levels": 1}, {"sample_shift": 12}])
+@pytest.mark.parametrize("knobs", [{}, {"bucket_levels": 1}, {"bucket_levels": 3}, {"sample_shift": 12},
+                                   {"sample_shift": 12, "bucket_levels": 3}])
 def test_bucketed_fold_many_slices(odd, knobs):
     """The bucketed signed fold (round 5) over 2^22 ids (8 slices of 2^19), a kron stream mapped bipartite: the same
     words as the unbucketed giant kernel and the oracle's success flag; with one odd edge (two even hub ids) placed

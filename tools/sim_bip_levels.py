@@ -29,3 +29,10 @@ e2=M[sv]
 print('level2 (by target) emitted',e2.sum(),'slow',(~e2).sum())
 e2s=M[su]
 print('level2 (by source) emitted',e2s.sum())
+# a third level, by the source again (the level-2 slow list swapped back)
+N2=np.zeros(V,bool); N2[su[e2]]=True
+M2=M|N2
+s2u,s2v=su[~e2],sv[~e2]
+e3=M2[s2u]
+print('level3 (by source) emitted',e3.sum(),'slow',(~e3).sum())
+in_giant=np.zeros(V,bool)
