@@ -8,18 +8,21 @@
 // 64-B line fetches bound it (1.7 misses per edge). Here both lookups find their slice of the snapshot in LDS:
 //   sb_filter_kernel   per source-slice bucket, the slice's 2 bits per id in LDS (128 KiB): u in C -> the pair
 //                      (v, parity(u) ^ 1) joins the EMIT list (v must carry that parity); else the edge joins the SLOW
-//                      list with its ends swapped (block-aggregated appends: one global add per list per 4K entries)
-//   bucket_kernel      the emit list split by v's slice (the same P1)
+//                      list with its ends swapped (block-aggregated appends: one global add per list per 16K
+//                      entries), and counts both lists' entries per slice of their first id (the next P1's exact layout)
+//   bucket_kernel      the emit list split by v's slice (the same P1, KEYONLY: 4-B entries, v's slice-local bits |
+//                      parity << 19)
 //   sb_check_kernel    per target-slice bucket, the slice in LDS: v in C -> its parity must be the pair's, else the
 //                      batch has an odd cycle (fail); v not in C -> v joins the block's LDS copy with that parity (a
 //                      lane that finds it added with the other parity: fail); at the end of its items a block ORs
 //                      its new members into N2, 2 bits per id: "reached with parity 0", "with parity 1"
+//   sb_join_low_kernel the new members below r united with r first (each makes C's root a smaller id)
 //   sb_join_kernel     C |= N2 (both parities: fail); a new member already seen in the forest (the sample's fold made
-//                      it seen in another tree), or below r, is united with r with its parity; the others stay
-//                      UNSEEN in the forest — DEFERRED, as the CC fold's N (bucket_join_kernel)
-// then the same again over the slow list against C | N (a second level) — by the edges' OTHER ends: a bipartite
-// stream's sources and targets can be disjoint sets (to_bipartite: even -> odd ids), and N holds targets — and the
-// remaining edges by
+//                      it seen in another tree) is united with C's root R (found once per block) with its parity; the
+//                      others stay UNSEEN in the forest — DEFERRED, as the CC fold's N (bucket_join_kernel)
+// then the same again over the slow list against C | N (a second level; `levels`: up to 3) — by the edges' OTHER ends:
+// a bipartite stream's sources and targets can be disjoint sets (to_bipartite: even -> odd ids), and N holds targets —
+// and the remaining edges by
 //   sb_rest_kernel     the giant kernel's rule with deferred members: an edge with one end x outside C unites x with
 //                      r (never with the deferred end itself); neither end in C: the signed union
 //   sb_compress_kernel the closing compress: a member of C is labelled (root(r) << 1) | (its parity ^ r's parity to
