@@ -23,6 +23,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -70,6 +71,8 @@ def parse():
     ap.add_argument("--tune", default="", help="fold-pipeline knobs k=v,... (gcc_forest_tune; speed only)")
     ap.add_argument("--phase-timing", choices=["timed", "after", "off"], default="after",
                     help="per-kernel dispatch events in the timed steps, in extra steps after them, or not at all")
+    ap.add_argument("--step-marker", action="store_true",
+                    help="launch gcc_step_mark_kernel once per step (rocprofv3 runs count steps by it)")
     return ap.parse_args()
 
 
@@ -123,19 +126,33 @@ def pmc_kernel_match(label, kname):
     return got.startswith(targs.rstrip(">").replace(" ", ""))
 
 
+def record_order(fname):
+    """Sort key of a profiles/ file by when it was recorded: the session tag r<round><letters><n> of its name (a..z,
+    aa..az, ba.. within a round: longer tags are later, so 'r5ba' > 'r5k'), then the record's own
+    'recorded' sequence number for records written since round 6."""
+    m = re.match(r"r(\d+)([a-z]*)(\d*)", fname)
+    if not m:
+        return (-1, 0, "", 0)
+    return (int(m.group(1)), len(m.group(2)), m.group(2), int(m.group(3) or 0))
+
+
 def profile_record(workload, kernel=None, units=None):
     """The newest committed rocprofv3 PMC summary for this workload (profiles/*_pmc_<workload>*.json) whose kernel is
-    `kernel` and whose units per launch match `units` (within 1 %), or None."""
+    `kernel` and whose units per launch match `units` (within 1 %), or None. Newest = the latest session tag
+    (record_order), and within one tag the highest 'recorded' field (tools/pmc_summary.py writes it)."""
     pdir = os.path.join(ROOT, "profiles")
     if not os.path.isdir(pdir):
         return None
-    for f in sorted(os.listdir(pdir), reverse=True):
+    cands = []
+    for f in os.listdir(pdir):
         if f"_pmc_{workload}" not in f or not f.endswith(".json"):
             continue
         try:
             rec = json.load(open(os.path.join(pdir, f)))
         except Exception:
             continue
+        cands.append((record_order(f) + (float(rec.get("recorded", 0)),), f, rec))
+    for _, f, rec in sorted(cands, key=lambda c: c[0], reverse=True):
         if kernel and not pmc_kernel_match(kernel, rec.get("kernel", "")):
             continue
         if units is not None and abs(rec.get("edges_per_launch", 0) - units) > 0.01 * max(1, units):
@@ -650,7 +667,16 @@ def main():
     host_fold_s = []
     merge_events = []  # (before merge, after merge) on the forest's stream, N > 1, instrumented steps only
 
+    mark = None
+    if args.step_marker:
+        from gelly_stream.native import call as native_call
+
+        def mark():
+            native_call("gcc_step_mark", stream.cuda_stream)
+
     def step(instrument):
+        if mark is not None:
+            mark()
         forest.ds.reset()
         for w in range(n_windows):
             o, n = offs[w]

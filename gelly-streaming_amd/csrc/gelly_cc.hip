@@ -1929,6 +1929,9 @@ __global__ __launch_bounds__(kBlock) void gen_kernel(gcc_gen_params prm, u64 fir
     }
 }
 
+// gcc_step_mark: an empty kernel that profilers count as the bench's once-per-step marker
+__global__ void gcc_step_mark_kernel() {}
+
 static inline unsigned grid_for(u64 n, unsigned max_blocks) {
     u64 b = (n + kBlock - 1) / kBlock;
     if (b < 1) b = 1;
@@ -2048,6 +2051,17 @@ struct FoldTune {
     // 2.7 ms): the recording fold with the touched marks, the resolve and the scan sharing the CUs with the next fold
     // cost more than the overlap returns
     int inc_pipe = 0;
+    // Lazy emission (round 6, VERDICT r5 next-4: short windows). gcc_forest_compress is the per-window emission
+    // (Merger.flatMap emits the running summary, …/SummaryAggregation.java:107-111). The emitted summary is the forest
+    // itself, as in the reference (DisjointSet.getMatches exposes the parent map and find compresses lazily,
+    // …/summaries/DisjointSet.java:49-51, :71-85): every root is its component's minimum id, so find(v) is exact on it.
+    // The emission compresses on every emit_every-th call only (and whenever a read needs the labels: labels, find,
+    // size, digest, serialize, a merge message), so a window pays its fold plus 1/emit_every of a compress. 1 = every
+    // emission compresses (rounds 1-5).
+    int emit_every = 1;
+    // the plain folds between lazy emissions: record their mutations for an incremental compress (1) or split paths
+    // and leave the compress that follows full (0)
+    int emit_rec = 1;
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -2174,6 +2188,7 @@ struct gcc_forest {
     std::vector<u32> slow_rounds;
 
     FoldTune tune;
+    u32 lazy_emits = 0;  // emissions since the last compress that left the forest as the summary (tune emit_every)
 
     u32 nwords() const { return (u32)(((u64)cap + 63) / 64); }
     bool filter_enabled() const { return tune.filter && cap >= kFilterMinIds; }
@@ -2568,6 +2583,7 @@ static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth =
     if (!inplace) std::swap(h->d_parent, h->d_spare);
     h->compressed = true;
     h->rec_all = inc_here && h->d_bloom;  // parent[] is compressed and the next fold's bloom is clear
+    h->lazy_emits = 0;
     return GCC_OK;
 }
 
@@ -2595,7 +2611,10 @@ static int refresh_now(gcc_forest* h) {
 static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* name) {
     if (n == 0) return GCC_OK;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
-    if (h->rec_all && n * std::max<u64>(1, h->tune.inc_div) <= (u64)h->cap) {
+    // the recording fold: every mutation since the last compress recorded, a short window of a big forest, and (lazy
+    // emission with emit_rec = 0: the folds between compresses split paths instead) recording wanted
+    if (h->rec_all && n * std::max<u64>(1, h->tune.inc_div) <= (u64)h->cap &&
+        (h->tune.emit_every <= 1 || h->tune.emit_rec)) {
         if (pipe_applies(h)) return pipe_fold(h, edges, n);
         int rc = pipe_exit(h);
         if (rc) return rc;
@@ -3765,6 +3784,7 @@ int gcc_forest_reset(gcc_forest* h) {
     h->compressed = true;  // all UNSEEN is canonical
     h->has_giant = false;  // the giant bitmap described the old forest
     h->filter_off = false;
+    h->lazy_emits = 0;
     return GCC_OK;
 }
 
@@ -4234,6 +4254,9 @@ int gcc_forest_deserialize(gcc_forest* h, const void* in, uint64_t size) {
 int gcc_forest_compress(gcc_forest* h) {
     CHECK_ARG(h, "null forest");
     DeviceGuard g(h->device);
+    // lazy emission (FoldTune::emit_every): the forest is the emitted summary until every emit_every-th emission
+    if (h->tune.emit_every > 1 && !h->pipe && !h->compressed && ++h->lazy_emits < (u32)h->tune.emit_every)
+        return flush_fold(h);
     return compress_async(h, false);
 }
 
@@ -4351,6 +4374,8 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "compress_split") t.compress_split = value != 0;
     else if (k == "fold_split") t.fold_split = value != 0;
     else if (k == "inc_pipe") t.inc_pipe = std::max(0, std::min(2, (int)value));
+    else if (k == "emit_every") t.emit_every = std::max(1, std::min(1 << 20, (int)value));
+    else if (k == "emit_rec") t.emit_rec = value != 0;
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
@@ -4433,6 +4458,12 @@ int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size) {
     h->slow_rounds.clear();
     if (out.size() + 1 > size) return set_err(GCC_E_INVALID, "profile buffer too small (%zu bytes needed)", out.size() + 1);
     snprintf(buf, size, "%s", out.c_str());
+    return GCC_OK;
+}
+
+int gcc_step_mark(void* hip_stream) {
+    hipLaunchKernelGGL(gcc_step_mark_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(hip_stream));
+    HIP_TRY(hipGetLastError());
     return GCC_OK;
 }
 

@@ -101,6 +101,7 @@ _SIGS = {
     "gcc_forest_enable_timing": (c_int, [c_void_p, c_int]),
     "gcc_forest_last_fold_ms": (c_int, [c_void_p, POINTER(c_float)]),
     "gcc_forest_fold_profile": (c_int, [c_void_p, c_char_p, c_uint64]),
+    "gcc_step_mark": (c_int, [c_void_p]),
     "gcc_forest_tune": (c_int, [c_void_p, c_char_p, ctypes.c_double]),
     "gcc_forest_label_digest": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),
     "gcc_forest_inc_check_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)]),

@@ -278,6 +278,10 @@ int gcc_forest_last_fold_ms(gcc_forest* h, float* ms);
  * "phase ms edges" lines; each fold starts with a "begin" line (+ "slow_edges 0 n" lines in mode 2).
  * Recording never synchronises, so a timed region stays sync-free; this call synchronises. */
 int gcc_forest_fold_profile(gcc_forest* h, char* buf, uint64_t size);
+/* measurement only: one empty kernel (gcc_step_mark_kernel) on hip_stream (NULL = the null stream). bench.py
+ * --step-marker launches it once per step, so a rocprofv3 run counts its steps from that kernel's launches
+ * (tools/pmc_summary.py) instead of guessing them from a kernel whose launches per step vary. */
+int gcc_step_mark(void* hip_stream);
 /* diagnostics (tune key inc_check = 1): totals over this forest's checked incremental compresses: how many ran,
  * labels that differed from the roots of the forest the compress started from, bloom words whose LDS copy lacked a
  * mark that memory held. Checked compresses synchronise; never on in a timed region. */

@@ -1,8 +1,12 @@
 """Summarise rocprofv3 PMC passes (tools/pmc_passes.sh) into profiles/<tag>_pmc_<workload>.json.
 
 HBM bytes per launch of a kernel = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: FETCH_SIZE/WRITE_SIZE are KB, and on
-gfx950 FETCH_SIZE reports half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section). The 2x is
-exact for the 16-B/lane edge stream and uncalibrated for the random 4-B parent reads (an upper estimate there).
+gfx950 FETCH_SIZE tallies every L2 -> fabric read request (one whole 128-B line) as 64 B. Calibrated per access class
+in round 6 (tools/probe_fetch_cal.hip, profiles/r6a_fetch_calibration.txt): the 2x holds for the 16-B/lane stream AND
+for scattered 4-B reads (one 128-B request per line touched, in the full stream's time); WRITE_SIZE is exact for 4-B
+stores (32-B requests), atomics (64-B requests) and streaming stores. Infinity-Cache hits are counted as requests.
+Steps: the run's launches of gcc_step_mark_kernel (bench.py --step-marker, once per step; VERDICT r5 weak 7a: C3's
+fold launches 5 kernels per step, so counting the dominant kernel's launches undercounted its per-step traffic 5x).
 Usage: python tools/pmc_summary.py <pmc_dir> <workload> <kernel substring> <units_per_launch> <bytes_per_unit> <out.json>
 (units: edges for the edge kernels; bytes_per_unit: bench.py KERNEL_BYTES)"""
 import csv
@@ -52,10 +56,13 @@ def main():
     rec["all_kernels"] = {  # every kernel of the run: HBM bytes per launch (same correction)
         k: {"launches": len(f[k]), "hbm_bytes_per_launch": (2 * sum(f[k]) / len(f[k]) + (sum(w[k]) / len(w[k]) if w.get(k) else 0)) * 1024}
         for k in f}
-    # the whole step's HBM traffic: every kernel of the run except the generator and the label copies, per step
-    # (steps = the dominant kernel's launches: one per step; run bench with --no-extras so no other leg is counted)
-    steps = len(fv) / max(1, len(names))
-    skip = ("gen_kernel", "__amd_rocclr_copyBuffer")
+    # the whole step's HBM traffic: every kernel of the run except the generator, the label copies and the marker,
+    # per step (steps = the marker's launches; run bench with --no-extras --step-marker so no other leg is counted)
+    marks = [k for k in f if "gcc_step_mark_kernel" in k]
+    if not marks:
+        sys.exit("no gcc_step_mark_kernel launches in the run: run bench.py with --step-marker (tools/pmc_passes.sh)")
+    steps = float(sum(len(f[k]) for k in marks))
+    skip = ("gen_kernel", "__amd_rocclr_copyBuffer", "gcc_step_mark_kernel")
     per_step = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in rec["all_kernels"].items()
                    if not any(x in k for x in skip)) / max(1.0, steps)
     # the kernel's average duration in the run's kernel-trace pass (tools/pmc_passes.sh): bench.py compares it with
@@ -68,9 +75,14 @@ def main():
             calls = sum(int(r["Calls"]) for r in rows)
             rec["kernel_ms_at_pmc"] = sum(float(r["TotalDurationNs"]) for r in rows) / max(1, calls) / 1e6
             break
+    rec["steps"] = steps
+    rec["launches_per_step"] = {k: v["launches"] / steps for k, v in rec["all_kernels"].items()
+                                if not any(x in k for x in skip)}
     rec["pipeline_traffic_per_step"] = per_step
     rec["pipeline_algorithmic_per_step"] = 16.0 * edges
     rec["pipeline_traffic_ratio"] = per_step / (16.0 * edges)
+    import time
+    rec["recorded"] = time.time()  # bench.py profile_record: the newest record wins within a session tag
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
