@@ -411,9 +411,10 @@ def windows_leg(name, ds_factory, windows, steps, warmup, digest, V, workload_ke
         ds.reset()
         for w, (ptr, n) in enumerate(windows):
             ds.fold_device(ptr, n)
-            ds.compress()
+            ds.compress()  # the window's emission (lazy in the plain regime: tune emit_div)
             if check is not None:
                 check(w)
+        ds.labels_device()  # the stream's last summary materialised as canonical labels, inside the step
 
     for _ in range(warmup):
         step()
@@ -695,6 +696,7 @@ def main():
                     merge_events.append((ev1, ev2))
             else:
                 forest.compress()
+        forest.ds.labels_device()  # the stream's last summary as canonical labels (a lazy emission's deferred compress)
 
     for _ in range(args.warmup):
         step(False)
@@ -780,8 +782,8 @@ def main():
             "windows_per_step": n_windows,
             "parallelism": f"dp{world}",
             "partition": "rank r folds the r-th contiguous 1/N of every window (strong scaling of one stream)",
-            "merge": ("gcc_forest_group_merge: compact all_gather over RCCL (giant bitmap + others list; label all_gather "
-                      "fallback)"
+            "merge": ("gcc_forest_group_merge: delta all_gather over RCCL ((x, root) of the ids each rank's window changed) "
+                      "when every rank is armed, else compact (giant bitmap + others list; label all_gather fallback)"
                       if world > 1 else "none"),
         },
         "roofline": roofline,
@@ -792,6 +794,8 @@ def main():
                    "message_bytes": group.last.get("bytes"),
                    "gathered_bytes_per_window": (group.last.get("bytes") or 0) * world,
                    "all_gathers_last_window": group.last.get("rounds"), "label_exchange": group.last.get("labels"),
+                   "kind_last_window": group.last.get("kind"),
+                   "bytes_all_rounds_last_window": group.last.get("bytes_all_rounds"),
                    "full_label_bytes": 4 * V,
                    "timing": "torch events around gcc_forest_group_merge on the forest's stream, instrumented steps"}
                   if group is not None and merge_ms else None),

@@ -117,23 +117,74 @@ __device__ __forceinline__ void trace_start(u32 id) {
     }
 }
 
+// The delta merge's lists (round 6; gcc_forest_encode_delta): kDeltaStripes stripes of `subcap` ids
+// each; cnt[s] = the ids stripe s has taken (it may run past subcap: then the delta is unusable and the merge takes the
+// compact message), cnt[kDeltaStripes] = some lane had more events than its slots. A wave appends its lanes' events to
+// stripe (its global wave index mod kDeltaStripes) with ONE atomicAdd: a per-event atomic on one counter would
+// serialise at the memory side (round 1's encode: 16K same-address atomics took 476 us).
+constexpr u32 kDeltaStripes = 64;
+struct DeltaLists {
+    u32* ids;
+    u32* cnt;
+    u32 subcap;
+};
+
+__device__ __forceinline__ void delta_append(const DeltaLists& d, const gcc::LaneEvents& ev) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 k = min(ev.n, gcc::kLaneEvents);
+    if (ev.n > gcc::kLaneEvents) atomicOr(&d.cnt[kDeltaStripes], 1u);
+    u32 incl = k;
+    for (int off = 1; off < 64; off <<= 1) {
+        const u32 y = __shfl_up(incl, off, 64);
+        if (lane >= (u32)off) incl += y;
+    }
+    const u32 total = __shfl(incl, 63, 64);
+    if (total == 0) return;
+    const u32 stripe = (blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) & (kDeltaStripes - 1);
+    u32 base = 0;
+    if (lane == 63) base = atomicAdd(&d.cnt[stripe], total);
+    base = __shfl(base, 63, 64);
+    u32* out = d.ids + (size_t)stripe * d.subcap;
+    u32 pos = base + incl - k;
+    for (u32 j = 0; j < k; ++j, ++pos)
+        if (pos < d.subcap) out[pos] = ev.x[j];
+}
+
 // SPLIT: path splitting in the finds (plain stores). END: 0 nothing; 1 every block ends with an agent-scope release
 // (its XCD's dirty L2 lines written back before the kernel ends); 2 every wave ends with s_waitcnt vmcnt(0) (its
 // stores and atomics acknowledged before it ends). A/B knobs of the recording fold (tune inc_split / fold_release).
-template <bool REC, bool SPLIT = true, int END = 0>
+// DELTA: every hooked root and new id also goes into the delta lists (the delta merge; the loop's trip count is then
+// wave-uniform, so the wave can aggregate its events).
+template <bool REC, bool SPLIT = true, int END = 0, bool DELTA = false>
 __global__ __launch_bounds__(kBlock) void fold_kernel(u32* __restrict__ parent, const u64* __restrict__ edges,
                                                       u64 n_edges, u32* __restrict__ bloom, u32 cap,
-                                                      u32* __restrict__ err) {
+                                                      u32* __restrict__ err, DeltaLists dl) {
     trace_start(kTrFold);
     NoCount c;
     typedef gcc::UnionFind<gcc::LoadPlain, SPLIT> U;
     const u64 stride = (u64)gridDim.x * kBlock;
-    for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n_edges; i += stride) {
-        const u64 e = __builtin_nontemporal_load(edges + i);
-        u32 a = (u32)e, b = (u32)(e >> 32);
-        if (!edge_ok(a, b, cap, err)) continue;
-        if constexpr (REC) U::unite(parent, a, b, c, gcc::BloomRec{bloom});
-        else U::unite(parent, a, b, c);
+    if constexpr (DELTA) {
+        for (u64 b0 = (u64)blockIdx.x * kBlock; b0 < n_edges; b0 += stride) {
+            const u64 i = b0 + threadIdx.x;
+            gcc::LaneEvents ev;
+            if (i < n_edges) {
+                const u64 e = __builtin_nontemporal_load(edges + i);
+                u32 a = (u32)e, b = (u32)(e >> 32);
+                if (edge_ok(a, b, cap, err)) {
+                    if constexpr (REC) U::unite(parent, a, b, c, gcc::BloomDeltaRec{bloom, &ev});
+                    else U::unite(parent, a, b, c, gcc::DeltaRec{&ev});
+                }
+            }
+            delta_append(dl, ev);
+        }
+    } else {
+        for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n_edges; i += stride) {
+            const u64 e = __builtin_nontemporal_load(edges + i);
+            u32 a = (u32)e, b = (u32)(e >> 32);
+            if (!edge_ok(a, b, cap, err)) continue;
+            if constexpr (REC) U::unite(parent, a, b, c, gcc::BloomRec{bloom});
+            else U::unite(parent, a, b, c);
+        }
     }
     if constexpr (END == 1) {
         __syncthreads();
@@ -1838,6 +1889,91 @@ __global__ __launch_bounds__(kBlock) void msg_absorb_kernel(u32* __restrict__ pa
     }
 }
 
+// ---- the delta merge's message (round 6; include/gelly_cc.h "delta message") ----------------------
+// u32 header[4] = {edges the sender folded since it armed, n_pairs (true count), id_capacity, status}, then n_pairs
+// (x, root(x)) pairs: one per id of the sender's delta lists, its root found in the sender's forest (read-only finds).
+// Every block loads the stripes' counts and their prefix (wave 0), then the flat index over the pairs maps to a stripe
+// by binary search: one kernel, no global atomics.
+__global__ __launch_bounds__(kBlock) void delta_encode_kernel(const u32* __restrict__ parent, const u32* __restrict__ ids,
+                                                              const u32* __restrict__ cnt, u32 subcap,
+                                                              u32* __restrict__ msg, u64 cap, u32 n, u32 edges,
+                                                              u32 armed) {
+    __shared__ u32 s_pre[kDeltaStripes + 1];
+    __shared__ u32 s_bad;
+    if (threadIdx.x < 64) {
+        const u32 lane = threadIdx.x;
+        u32 k = armed ? cnt[lane] : 0;
+        const bool over = k > subcap;
+        k = min(k, subcap);
+        u32 incl = k;
+        for (int off = 1; off < 64; off <<= 1) {
+            const u32 y = __shfl_up(incl, off, 64);
+            if (lane >= (u32)off) incl += y;
+        }
+        s_pre[lane + 1] = incl;
+        const unsigned long long ob = __ballot(over);
+        if (lane == 0) {
+            s_pre[0] = 0;
+            s_bad = (ob != 0 || (armed && cnt[kDeltaStripes] != 0)) ? 1u : 0u;
+        }
+    }
+    __syncthreads();
+    const u32 total = s_pre[kDeltaStripes];
+    const u32 status = !armed ? GCC_DELTA_STATUS_UNARMED : (s_bad ? GCC_DELTA_STATUS_OVERFLOW : 0u);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        msg[0] = edges;
+        msg[1] = total;
+        msg[2] = n;
+        msg[3] = status;
+    }
+    if (status) return;
+    u32* pairs = msg + GCC_MSG_HEADER_BYTES / sizeof(u32);
+    const u64 end = min((u64)total, cap);
+    for (u64 t = (u64)blockIdx.x * kBlock + threadIdx.x; t < end; t += (u64)gridDim.x * kBlock) {
+        u32 lo = 0, hi = kDeltaStripes;  // the last stripe s with s_pre[s] <= t (a non-empty one)
+        while (hi - lo > 1) {
+            const u32 mid = (lo + hi) >> 1;
+            if (s_pre[mid] <= (u32)t) lo = mid;
+            else hi = mid;
+        }
+        const u32 x = ids[(size_t)lo * subcap + ((u32)t - s_pre[lo])];
+        NoCount c;
+        const u32 p = parent[x];
+        pairs[2 * t] = x;
+        pairs[2 * t + 1] = (p >= x) ? x : UFRead::find_from(const_cast<u32*>(parent), x, p, c);
+    }
+}
+
+// Absorb the peers' delta messages: unite(x, r) for every pair, one pair per lane over a flat (peer, pair) index. The
+// unions write parent[] with memory-side atomics only (UFRec) and, when every mutation since the last compress was
+// recorded (bloom != null), mark their hooks in the incremental compress's bloom, so that compress stays incremental.
+// Block 0 also zeroes this forest's own stripe counters (the encode read them one kernel before): the delta is armed
+// again from here (the merge is complete once this kernel has run).
+template <bool BLOOM>
+__global__ __launch_bounds__(kBlock) void delta_absorb_kernel(u32* __restrict__ parent, const char* __restrict__ msgs,
+                                                              u64 stride, u32 count, u32 skip, u64 cap, u32 n,
+                                                              u32* __restrict__ bloom, u32* __restrict__ own_cnt,
+                                                              u32* __restrict__ err) {
+    if (blockIdx.x == 0 && own_cnt && threadIdx.x <= kDeltaStripes) atomicExch(&own_cnt[threadIdx.x], 0u);
+    NoCount c;
+    const u64 stride_t = (u64)gridDim.x * kBlock;
+    for (u64 t = (u64)blockIdx.x * kBlock + threadIdx.x; t < (u64)count * cap; t += stride_t) {
+        const u32 p = (u32)(t / cap);
+        const u64 k = t - (u64)p * cap;
+        if (p == skip) continue;
+        const u32* hdr = reinterpret_cast<const u32*>(msgs + p * stride);
+        if (hdr[2] != n || hdr[3] != 0 || k >= min((u64)hdr[1], cap)) continue;
+        const u32* pairs = hdr + GCC_MSG_HEADER_BYTES / sizeof(u32);
+        const u32 x = pairs[2 * k], r = pairs[2 * k + 1];
+        if (x >= n || r >= n) {
+            *err = 1u;
+            continue;
+        }
+        if constexpr (BLOOM) gcc::UFRec::unite(parent, x, r, c, gcc::BloomRec{bloom});
+        else gcc::UFRec::unite(parent, x, r, c);
+    }
+}
+
 #include "bucket_fold.h"
 #include "signed_bucket.h"  // the signed forest's bucketed fold (gelly_bip.hip), reusing bucket_fold.h's P1
 #include "signed_bucket_api.h"
@@ -2055,13 +2191,19 @@ struct FoldTune {
     // (Merger.flatMap emits the running summary, …/SummaryAggregation.java:107-111). The emitted summary is the forest
     // itself, as in the reference (DisjointSet.getMatches exposes the parent map and find compresses lazily,
     // …/summaries/DisjointSet.java:49-51, :71-85): every root is its component's minimum id, so find(v) is exact on it.
-    // The emission compresses on every emit_every-th call only (and whenever a read needs the labels: labels, find,
-    // size, digest, serialize, a merge message), so a window pays its fold plus 1/emit_every of a compress. 1 = every
-    // emission compresses (rounds 1-5).
-    int emit_every = 1;
+    // In the plain regime (no tracked giant: C3, C5) the emission compresses only once the edges folded since the last
+    // compress reach id_capacity / emit_div (and whenever a read needs the labels: labels, find, size, digest,
+    // serialize, a merge message), so a window pays its fold plus an amortised O(1) per edge for the O(id_capacity)
+    // compress, not an O(id_capacity) scan per window. 0 = every emission compresses (rounds 1-5).
+    // Measured on C5 (256 windows of 2^16 edges; profiles/r6c_*, every window's emitted forest bit-exact): a compress
+    // every 4 / 8 / 16 / 32 windows: 3.70 / 4.22 / 4.55 / 4.78 G edges/s (recording folds + incremental compress), 4.55 /
+    // 5.25 G at 16 / 32 with splitting folds + full compress, against 2.08 eager. The giant-filtered regime (C2) keeps
+    // the eager emission: its compress refreshes the filter's bitmap (lazy there measured slower: C2 x 16 at 4 / 8
+    // windows 0.296 / 0.417 ms against 0.259).
+    int emit_div = 8;
     // the plain folds between lazy emissions: record their mutations for an incremental compress (1) or split paths
-    // and leave the compress that follows full (0)
-    int emit_rec = 1;
+    // and leave the compress that follows full (0: measured faster at C5's 32 windows per compress)
+    int emit_rec = 0;
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -2187,8 +2329,20 @@ struct gcc_forest {
     u32* h_segcount = nullptr;  // pinned copies of the slow-queue segment counts, one row per filtered round
     std::vector<u32> slow_rounds;
 
+    // the delta merge (round 6): while armed (gcc_forest_delta_arm, after a group merge), every plain fold
+    // also lists the ids it changes (fold_kernel<.., DELTA>) in kDeltaStripes stripes of delta_subcap ids; any other
+    // mutation disarms it. delta_need: the per-stripe worst case of the folds since arming (the lists are grown before a
+    // fold that could overflow them); delta_edges: the edges folded since arming (the message header's)
+    bool delta_armed = false;
+    bool delta_cnt_zero = false;  // the stripe counters are known to be zero (memset, or zeroed by the delta absorb)
+    u32* d_delta = nullptr;
+    u32* d_delta_cnt = nullptr;  // kDeltaStripes counters + the lane-overflow flag
+    u32 delta_subcap = 0;
+    u64 delta_need = 0;
+    u64 delta_edges = 0;
+
     FoldTune tune;
-    u32 lazy_emits = 0;  // emissions since the last compress that left the forest as the summary (tune emit_every)
+    u64 edges_since_compress = 0;  // lazy emission (FoldTune::emit_div)
 
     u32 nwords() const { return (u32)(((u64)cap + 63) / 64); }
     bool filter_enabled() const { return tune.filter && cap >= kFilterMinIds; }
@@ -2213,6 +2367,7 @@ static void mark_mutated(gcc_forest* h, bool recorded = false) {
     ++h->version;
     h->compressed = false;
     if (!recorded) {
+        h->delta_armed = false;  // a mutation the delta lists did not see
         h->rec_all = false;
         h->pipe_roots_stale = true;  // conservatively: the pipelined emission's roots arrays start from UNSEEN again
     }
@@ -2318,6 +2473,7 @@ static int stream_sync_checked(gcc_forest* h) {
 static int materialize_reset(gcc_forest* h) {
     if (!h->pending_reset) return GCC_OK;
     h->rec_all = false;
+    h->delta_armed = false;
     HIP_TRY(hipMemsetAsync(h->d_parent, 0xFF, (size_t)h->cap * sizeof(u32), h->stream));
     h->pending_reset = false;
     return GCC_OK;
@@ -2583,7 +2739,7 @@ static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth =
     if (!inplace) std::swap(h->d_parent, h->d_spare);
     h->compressed = true;
     h->rec_all = inc_here && h->d_bloom;  // parent[] is compressed and the next fold's bloom is clear
-    h->lazy_emits = 0;
+    h->edges_since_compress = 0;
     return GCC_OK;
 }
 
@@ -2608,20 +2764,62 @@ static int refresh_now(gcc_forest* h) {
     return GCC_OK;
 }
 
+// The delta lists must hold the worst case of this fold on top of what they hold (a wave appends at most
+// kLaneEvents ids per lane per iteration into its stripe): grown here, before the launch, if they could overflow.
+static int delta_reserve(gcc_forest* h, u64 n, u32 grid) {
+    const u64 waves = (u64)grid * (kBlock / 64);
+    const u64 iters = (n + (u64)grid * kBlock - 1) / ((u64)grid * kBlock);
+    const u64 need = h->delta_need + (waves + kDeltaStripes - 1) / kDeltaStripes * iters * 64 * gcc::kLaneEvents;
+    if (need > (1ull << 26)) {  // past 4G ids of lists: this window takes the compact message
+        h->delta_armed = false;
+        return GCC_OK;
+    }
+    if (need > h->delta_subcap) {
+        const u64 nc = std::max<u64>({need, 2ull * h->delta_subcap, 1024});
+        u32* nb = nullptr;
+        HIP_TRY(hipMalloc((void**)&nb, (size_t)kDeltaStripes * nc * sizeof(u32)));
+        if (h->d_delta) {
+            if (h->delta_need)
+                HIP_TRY(hipMemcpy2DAsync(nb, nc * sizeof(u32), h->d_delta, (size_t)h->delta_subcap * sizeof(u32),
+                                         (size_t)h->delta_subcap * sizeof(u32), kDeltaStripes, hipMemcpyDeviceToDevice,
+                                         h->stream));
+            HIP_TRY(hipStreamSynchronize(h->stream));  // (growth only: the old lists may still be read)
+            HIP_TRY(hipFree(h->d_delta));
+        }
+        h->d_delta = nb;
+        h->delta_subcap = (u32)nc;
+    }
+    h->delta_need = need;
+    h->delta_edges += n;
+    h->delta_cnt_zero = false;
+    return GCC_OK;
+}
+
 static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* name) {
     if (n == 0) return GCC_OK;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
     // the recording fold: every mutation since the last compress recorded, a short window of a big forest, and (lazy
     // emission with emit_rec = 0: the folds between compresses split paths instead) recording wanted
-    if (h->rec_all && n * std::max<u64>(1, h->tune.inc_div) <= (u64)h->cap &&
-        (h->tune.emit_every <= 1 || h->tune.emit_rec)) {
-        if (pipe_applies(h)) return pipe_fold(h, edges, n);
-        int rc = pipe_exit(h);
-        if (rc) return rc;
-        const dim3 g(grid_for(n, kMaxGrid));
+    const bool rec = h->rec_all && n * std::max<u64>(1, h->tune.inc_div) <= (u64)h->cap &&
+                     (h->tune.emit_div <= 0 || h->tune.emit_rec);
+    if (rec && pipe_applies(h)) {
+        h->delta_armed = false;  // the pipelined fold keeps no delta lists
+        return pipe_fold(h, edges, n);
+    }
+    int rc = pipe_exit(h);
+    if (rc) return rc;
+    const dim3 g(grid_for(n, kMaxGrid));
+    if (h->delta_armed && (rc = delta_reserve(h, n, g.x))) return rc;
+    const bool delta = h->delta_armed;
+    const DeltaLists dl{h->d_delta, h->d_delta_cnt, h->delta_subcap};
+    if (rec) {
         u32* bl = h->bloom(h->bloom_cur);
         const int v = (h->tune.inc_split ? 0 : 1) + 2 * std::max(0, std::min(2, h->tune.fold_release));
-#define GCC_REC(S, E) launch_k(h, name, n, fold_kernel<true, S, E>, g, dim3(kBlock), 0, h->d_parent, edges, n, bl, h->cap, h->d_err)
+        if (delta && v == 1)
+            return launch_k(h, name, n, fold_kernel<true, false, 0, true>, g, dim3(kBlock), 0, h->d_parent, edges, n, bl,
+                            h->cap, h->d_err, dl);
+        h->delta_armed = false;  // the A/B variants below keep no delta lists
+#define GCC_REC(S, E) launch_k(h, name, n, fold_kernel<true, S, E>, g, dim3(kBlock), 0, h->d_parent, edges, n, bl, h->cap, h->d_err, DeltaLists{})
         switch (v) {
         case 0: return GCC_REC(true, 0);
         case 1: return GCC_REC(false, 0);
@@ -2632,20 +2830,23 @@ static int launch_plain(gcc_forest* h, const u32* d_pairs, u64 n, const char* na
         }
 #undef GCC_REC
     }
-    int rc = pipe_exit(h);
-    if (rc) return rc;
     h->rec_all = false;
     if (!h->tune.fold_split)  // read-only finds in the plain fold too (A/B, round 5: the compress measured faster so)
-        return launch_k(h, name, n, fold_kernel<false, false>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent,
-                        edges, n, (u32*)nullptr, h->cap, h->d_err);
-    return launch_k(h, name, n, fold_kernel<false>, dim3(grid_for(n, kMaxGrid)), dim3(kBlock), 0, h->d_parent, edges, n,
-                    (u32*)nullptr, h->cap, h->d_err);
+        return delta ? launch_k(h, name, n, fold_kernel<false, false, 0, true>, g, dim3(kBlock), 0, h->d_parent, edges, n,
+                                (u32*)nullptr, h->cap, h->d_err, dl)
+                     : launch_k(h, name, n, fold_kernel<false, false>, g, dim3(kBlock), 0, h->d_parent, edges, n,
+                                (u32*)nullptr, h->cap, h->d_err, DeltaLists{});
+    return delta ? launch_k(h, name, n, fold_kernel<false, true, 0, true>, g, dim3(kBlock), 0, h->d_parent, edges, n,
+                            (u32*)nullptr, h->cap, h->d_err, dl)
+                 : launch_k(h, name, n, fold_kernel<false>, g, dim3(kBlock), 0, h->d_parent, edges, n, (u32*)nullptr,
+                            h->cap, h->d_err, DeltaLists{});
 }
 
 static int launch_filtered(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (n == 0) return GCC_OK;
     if (int rc = pipe_exit(h)) return rc;
     h->rec_all = false;  // the filtered fold does not record its mutations
+    h->delta_armed = false;  // nor list them for the delta merge
     const u32 nw = h->nwords() + (h->nwords() & 1);  // u64 bitmap words, rounded to 16 B
     const bool lds = nw <= kLdsBitmapMaxWords && (double)n >= h->tune.lds_edges_per_word * (double)nw;
     const u32 nblocks = lds ? (u32)h->n_cu : kMaxGrid;
@@ -2702,6 +2903,7 @@ static int launch_seed(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (int rc = pipe_exit(h)) return rc;
     const FoldTune& t = h->tune;
     h->rec_all = false;
+    h->delta_armed = false;
     int rc = alloc_filter(h);
     if (rc) return rc;
     const u64* edges = reinterpret_cast<const u64*>(d_pairs);
@@ -3114,6 +3316,7 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
 static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
     if (n == 0) return GCC_OK;
     const FoldTune& t = h->tune;
+    h->edges_since_compress += n;
     const int ev_first = (int)h->kev_used;
     if (h->timing) h->klog.push_back({"begin", -1, 0});
     int rc = GCC_OK;
@@ -3674,6 +3877,8 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (h->d_scratch) (void)hipFree(h->d_scratch);
     if (h->d_witness) (void)hipFree(h->d_witness);
     if (h->d_seg) (void)hipFree(h->d_seg);
+    if (h->d_delta) (void)hipFree(h->d_delta);
+    if (h->d_delta_cnt) (void)hipFree(h->d_delta_cnt);
     if (h->d_msg_oth) (void)hipFree(h->d_msg_oth);
     if (h->d_bits) (void)hipFree(h->d_bits);
     if (h->d_bloom) (void)hipFree(h->d_bloom);
@@ -3784,7 +3989,8 @@ int gcc_forest_reset(gcc_forest* h) {
     h->compressed = true;  // all UNSEEN is canonical
     h->has_giant = false;  // the giant bitmap described the old forest
     h->filter_off = false;
-    h->lazy_emits = 0;
+    h->edges_since_compress = 0;
+    h->delta_armed = false;
     return GCC_OK;
 }
 
@@ -3947,6 +4153,7 @@ int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* d_labels, u
     ++into->version;
     into->compressed = false;
     into->rec_all = false;
+    into->delta_armed = false;
     return GCC_OK;
 }
 
@@ -4126,6 +4333,66 @@ int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_by
     return GCC_OK;
 }
 
+// ---- the delta merge (round 6; include/gelly_cc.h) ---------------------------------------------------
+uint64_t gcc_delta_msg_bytes(uint64_t cap_pairs) { return GCC_MSG_HEADER_BYTES + 8 * cap_pairs; }
+
+int gcc_forest_delta_arm(gcc_forest* h) {
+    CHECK_ARG(h, "null forest");
+    DeviceGuard g(h->device);
+    int rc = flush(h);
+    if (rc) return rc;
+    if (!h->d_delta_cnt) HIP_TRY(hipMalloc((void**)&h->d_delta_cnt, (kDeltaStripes + 1) * sizeof(u32)));
+    if (!h->delta_cnt_zero) HIP_TRY(hipMemsetAsync(h->d_delta_cnt, 0, (kDeltaStripes + 1) * sizeof(u32), h->stream));
+    h->delta_cnt_zero = true;
+    h->delta_need = 0;
+    h->delta_edges = 0;
+    h->delta_armed = !h->pending_reset;  // a pending reset is a mutation no list records
+    return GCC_OK;
+}
+
+int gcc_forest_encode_delta(gcc_forest* h, void* d_msg, uint64_t cap_pairs) {
+    CHECK_ARG(h && d_msg, "null argument");
+    CHECK_ARG((reinterpret_cast<uintptr_t>(d_msg) & 15) == 0, "message buffer must be 16-byte aligned");
+    DeviceGuard g(h->device);
+    int rc = flush(h);
+    if (rc) return rc;
+    const bool armed = h->delta_armed && h->d_delta && h->d_delta_cnt;
+    const u64 bound = armed ? std::min<u64>(cap_pairs, (u64)kDeltaStripes * h->delta_subcap) : 0;
+    hipLaunchKernelGGL(delta_encode_kernel, dim3(grid_for(std::max<u64>(bound, 1), kMaxGrid)), dim3(kBlock), 0, h->stream,
+                       (const u32*)h->d_parent, (const u32*)h->d_delta, (const u32*)h->d_delta_cnt, h->delta_subcap,
+                       static_cast<u32*>(d_msg), (u64)cap_pairs, h->cap,
+                       (u32)std::min<u64>(h->delta_edges, 0xFFFFFFFFull), armed ? 1u : 0u);
+    return msg_launched(h, "delta_encode_kernel");
+}
+
+int gcc_forest_absorb_delta_many(gcc_forest* h, const void* d_msgs, uint64_t stride_bytes, uint32_t count, uint32_t skip,
+                                 uint64_t cap_pairs) {
+    CHECK_ARG(h && (d_msgs || count == 0), "null argument");
+    CHECK_ARG(((reinterpret_cast<uintptr_t>(d_msgs) | stride_bytes) & 15) == 0, "messages must be 16-byte aligned");
+    CHECK_ARG(count <= 1 || stride_bytes >= gcc_delta_msg_bytes(cap_pairs), "stride smaller than a message");
+    if (h->tune.fail_absorb > 0 && --h->tune.fail_absorb == 0)
+        return set_err(GCC_E_INTERNAL, "gcc_forest_absorb_delta_many: injected failure (tune key fail_absorb)");
+    DeviceGuard g(h->device);
+    int rc = flush(h);
+    if (rc) return rc;
+    // the unions keep the incremental compress's bloom complete when it is (rec_all): the next compress stays incremental
+    const bool bloom = h->rec_all && h->d_bloom && inc_forest(h);
+    const u64 work = std::max<u64>((u64)count * cap_pairs, 1);
+    if (bloom)
+        hipLaunchKernelGGL(delta_absorb_kernel<true>, dim3(grid_for(work, kMaxGrid)), dim3(kBlock), 0, h->stream, h->d_parent,
+                           static_cast<const char*>(d_msgs), (u64)stride_bytes, count, skip, (u64)cap_pairs, h->cap,
+                           h->bloom(h->bloom_cur), h->d_delta_cnt, h->d_err);
+    else
+        hipLaunchKernelGGL(delta_absorb_kernel<false>, dim3(grid_for(work, kMaxGrid)), dim3(kBlock), 0, h->stream,
+                           h->d_parent, static_cast<const char*>(d_msgs), (u64)stride_bytes, count, skip, (u64)cap_pairs,
+                           h->cap, (u32*)nullptr, h->d_delta_cnt, h->d_err);
+    if ((rc = msg_launched(h, "delta_absorb_kernel"))) return rc;
+    mark_mutated(h, bloom);
+    h->delta_armed = false;  // the caller arms it again once the merge is complete (gcc_forest_delta_arm)
+    if (h->d_delta_cnt) h->delta_cnt_zero = true;  // the absorb zeroed this forest's stripe counters
+    return GCC_OK;
+}
+
 int gcc_forest_absorb(gcc_forest* h, const void* d_msg, uint64_t cap_others) {
     return gcc_forest_absorb_many(h, d_msg, 0, 1, UINT32_MAX, cap_others);
 }
@@ -4254,8 +4521,10 @@ int gcc_forest_deserialize(gcc_forest* h, const void* in, uint64_t size) {
 int gcc_forest_compress(gcc_forest* h) {
     CHECK_ARG(h, "null forest");
     DeviceGuard g(h->device);
-    // lazy emission (FoldTune::emit_every): the forest is the emitted summary until every emit_every-th emission
-    if (h->tune.emit_every > 1 && !h->pipe && !h->compressed && ++h->lazy_emits < (u32)h->tune.emit_every)
+    // lazy emission (FoldTune::emit_div): in the plain regime the forest itself is the emitted summary until the edges
+    // folded since the last compress reach id_capacity / emit_div
+    if (h->tune.emit_div > 0 && !h->pipe && !h->compressed && (!h->filter_enabled() || h->filter_off) &&
+        h->edges_since_compress * (u64)h->tune.emit_div < (u64)h->cap)
         return flush_fold(h);
     return compress_async(h, false);
 }
@@ -4374,7 +4643,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "compress_split") t.compress_split = value != 0;
     else if (k == "fold_split") t.fold_split = value != 0;
     else if (k == "inc_pipe") t.inc_pipe = std::max(0, std::min(2, (int)value));
-    else if (k == "emit_every") t.emit_every = std::max(1, std::min(1 << 20, (int)value));
+    else if (k == "emit_div") t.emit_div = std::max(0, std::min(1 << 20, (int)value));
     else if (k == "emit_rec") t.emit_rec = value != 0;
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));

@@ -12,6 +12,14 @@
 // not fit, and then the exchange is repeated larger — exact, since union is idempotent. When the compact form is
 // not smaller than the label array (no dominant component) the label arrays themselves are all-gathered.
 //
+// Round 6: the DELTA merge first. After a merge every rank holds the same partition and arms its delta; its next
+// plain folds list the ids they change, so the next merge only needs (x, root(x)) for those: at most 2 pairs per edge
+// the rank folded in the window, like the reference's per-window partials (…/SummaryBulkAggregation.java:80-83: a
+// fresh partial per window, so the all-window reduce moves only that window's unions). One all_gather of the delta
+// messages (capacity: twice the largest window any rank reported last time); if any rank's delta is unusable (not
+// armed: its window took a fold the lists do not see; or overflowed) or larger than the capacity, the ranks fall back
+// to the compact rounds below, which are exact whatever was absorbed before (union is idempotent).
+//
 // Built only on the public C ABI of the forest (encode / absorb / labels / merge_labels / compress / stream) plus
 // HIP and RCCL. RCCL is resolved at run time with dlopen("librccl.so.1"): a process that already mapped one (torch
 // does) shares it, so there is exactly one RCCL per process.
@@ -127,6 +135,17 @@ struct gcc_comm {
     u64 last_bytes = 0;    // bytes each rank contributed to the last merge's all_gather
     int last_rounds = 0;   // all_gathers of the last merge (compact rounds + the label exchange)
     bool last_labels = false;  // the last merge ended with the label exchange
+    // the delta merge (round 6): its own buffers, the pair capacity (same on every rank: derived from the gathered
+    // headers) and how the last merge ended: 0 compact, 1 labels, 2 delta
+    void* d_dsend = nullptr;
+    u64 dsend_bytes = 0;
+    void* d_drecv = nullptr;
+    u64 drecv_bytes = 0;
+    u64 agreed_delta = 0;
+    u64 cap_delta = 0;
+    bool delta_off = false;  // GELLY_GROUP_DELTA=0: compact rounds only (A/B)
+    int last_kind = 0;
+    u64 last_total_bytes = 0;  // every all_gather of the last merge, bytes per rank summed
     // a merge failed where the ranks could not agree on it (e.g. a buffer allocation before the collective): the
     // communicator was aborted and is unusable; the peers may be left inside the collective, so the job's ranks must
     // all be torn down (as a failed Flink task restarts the job)
@@ -236,11 +255,72 @@ int merge_labels_rccl(gcc_forest* h, gcc_comm* c, u32 V, hipStream_t st, int loc
     if (r != ncclSuccess)
         return fail_comm(c, gcc_set_err(GCC_E_HIP, "ncclAllGather (labels): %s", rccl().GetErrorString(r)));
     c->last_bytes = 4ull * V;
+    c->last_total_bytes += 4ull * V;
     int rc2 = GCC_OK;
     for (int p = 0; p < c->nranks && !rc2; ++p)
         if (p != c->rank) rc2 = gcc_forest_merge_labels_device(h, static_cast<const u32*>(c->d_recv) + (u64)p * V, V);
     if (!rc2) rc2 = gcc_forest_compress(h);
+    if (!rc2) rc2 = gcc_forest_delta_arm(h);
     return rc2 ? own_error(c, rc2) : GCC_OK;
+}
+
+// The delta round (round 6). *done = true when the merge is complete (every rank absorbed every delta) or failed in
+// agreement (the return code says which); false: the ranks go on to the compact rounds (every rank takes that
+// decision from the same gathered headers). Every rank's forest stays valid either way.
+int delta_round(gcc_forest* h, gcc_comm* c, u32 V, hipStream_t st, int& local_rc, bool* done) {
+    *done = false;
+    const u64 cap = c->cap_delta;
+    const u64 size = round16(gcc_delta_msg_bytes(cap));
+    if (size > c->agreed_delta) {
+        int rc = ensure(c->d_dsend, c->dsend_bytes, size);
+        if (!rc) rc = ensure(c->d_drecv, c->drecv_bytes, (u64)c->nranks * size);
+        if (rc) c->agreed_delta = 0;
+        int failed = -1;
+        ABI_TRY(agree(c, st, rc ? rc : local_rc, &failed));
+        if (rc || failed >= 0) {
+            *done = true;
+            return agreed_error(rc ? rc : local_rc, failed);
+        }
+        c->agreed_delta = size;
+    }
+    if (!local_rc) local_rc = gcc_forest_encode_delta(h, c->d_dsend, cap);
+    if (local_rc) {
+        const u32 hdr[4] = {0, 0, 0, GCC_MSG_STATUS_FAILED};
+        int rc = hipMemcpyAsync(c->d_dsend, hdr, sizeof(hdr), hipMemcpyHostToDevice, st) == hipSuccess ? GCC_OK
+                 : gcc_set_err(GCC_E_HIP, "failed-status header copy");
+        if (!rc) rc = hipStreamSynchronize(st) == hipSuccess ? GCC_OK : gcc_set_err(GCC_E_HIP, "stream sync");
+        if (rc) return fail_comm(c, rc);
+    }
+    const ncclResult_t r = rccl().AllGather(c->d_dsend, c->d_drecv, (size_t)size, ncclUint8, c->comm, st);
+    if (r != ncclSuccess) return fail_comm(c, gcc_set_err(GCC_E_HIP, "ncclAllGather (deltas): %s", rccl().GetErrorString(r)));
+    ++c->last_rounds;
+    c->last_total_bytes += size;
+    if (hipMemcpy2DAsync(c->h_hdr, 16, c->d_drecv, (size_t)size, 16, (size_t)c->nranks, hipMemcpyDeviceToHost, st) !=
+            hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return fail_comm(c, gcc_set_err(GCC_E_HIP, "gathered delta headers: %s", hipGetErrorString(hipGetLastError())));
+    u64 nmax = 0, emax = 0;
+    bool usable = true;
+    for (int p = 0; p < c->nranks; ++p) {
+        const u32* hp = c->h_hdr + 4 * p;
+        if (hp[3] == GCC_MSG_STATUS_FAILED) {
+            *done = true;
+            return local_rc ? local_rc : gcc_set_err(GCC_E_INTERNAL, "group merge: rank %d failed (its error is on that rank)", p);
+        }
+        usable &= hp[3] == 0 && hp[2] == V;
+        nmax = std::max<u64>(nmax, hp[1]);
+        emax = std::max<u64>(emax, hp[0]);
+    }
+    // the next capacity: twice the largest window a rank folded (a bound: <= 2 pairs per edge), at least the pairs seen
+    c->cap_delta = std::max<u64>({1024, 2 * emax, nmax});
+    if (!usable || nmax > cap) return GCC_OK;  // the compact rounds (this one's all_gather is not wasted: see above)
+    if (!local_rc) local_rc = gcc_forest_absorb_delta_many(h, c->d_drecv, size, (u32)c->nranks, (u32)c->rank, cap);
+    if (!local_rc) local_rc = gcc_forest_delta_arm(h);
+    if (!local_rc) local_rc = gcc_forest_compress(h);  // the emission (lazy when the forest's emit_every says so)
+    c->last_bytes = size;
+    c->last_kind = 2;
+    *done = true;
+    return local_rc ? own_error(c, local_rc) : GCC_OK;
 }
 
 }  // namespace
@@ -306,6 +386,8 @@ int gcc_comm_destroy(gcc_comm* c) {
     DeviceGuard g(c->device);
     if (c->d_send) (void)hipFree(c->d_send);
     if (c->d_recv) (void)hipFree(c->d_recv);
+    if (c->d_dsend) (void)hipFree(c->d_dsend);
+    if (c->d_drecv) (void)hipFree(c->d_drecv);
     if (c->h_hdr) (void)hipHostFree(c->h_hdr);
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->h_status) (void)hipHostFree(c->h_status);
@@ -330,6 +412,14 @@ int gcc_comm_last_merge(gcc_comm* c, int* rounds, int* labels, uint64_t* cap_oth
     return GCC_OK;
 }
 
+int gcc_comm_last_merge_kind(gcc_comm* c, int* kind, uint64_t* bytes_per_rank, uint64_t* cap_delta) {
+    CHECK_ARG(c, "null comm");
+    if (kind) *kind = c->last_kind;
+    if (bytes_per_rank) *bytes_per_rank = c->last_total_bytes;
+    if (cap_delta) *cap_delta = c->cap_delta;
+    return GCC_OK;
+}
+
 // Collective: every rank calls it with its forest (same id_capacity everywhere); afterwards every rank's forest is
 // the union of all of them, compressed. Synchronises the forest's stream (it reads the gathered headers).
 int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
@@ -346,6 +436,8 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
     if (c->cap_others == 0) c->cap_others = std::max<u64>(1024, V / 64);
     c->last_rounds = 0;
     c->last_labels = false;
+    c->last_kind = 0;
+    c->last_total_bytes = 0;
     // Every rank takes the same decisions (sizes, repeats) from the gathered headers. A rank whose own encode, absorb
     // or compress fails keeps following them: in a next compact round it sends a failed-status header
     // (include/gelly_cc.h), before a round that grows the buffers and before the label exchange the ranks agree
@@ -353,6 +445,18 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
     int local_rc = c->poisoned ? gcc_set_err(GCC_E_INTERNAL, "an earlier group merge failed on this rank (its forest is "
                                                               "not the union of the ranks'): destroy the group")
                                : GCC_OK;
+    // the delta round first, while a delta message is smaller than the compact one (the same decision on every rank:
+    // both sizes come from values every rank holds)
+    if (c->cap_delta == 0) {
+        const char* e = getenv("GELLY_GROUP_DELTA");
+        c->delta_off = e && *e == '0';
+        c->cap_delta = 1024;
+    }
+    if (!c->delta_off && gcc_delta_msg_bytes(c->cap_delta) < std::min<u64>(gcc_msg_bytes(V, c->cap_others), 4ull * V)) {
+        bool done = false;
+        const int rc = delta_round(h, c, V, st, local_rc, &done);
+        if (done || rc) return rc;
+    }
     while (!c->prefer_labels) {
         const u64 cap = c->cap_others;
         const u64 size = round16(gcc_msg_bytes(V, cap));
@@ -391,6 +495,7 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
         if (!local_rc) local_rc = gcc_forest_compress(h);
         ++c->last_rounds;
         c->last_bytes = size;
+        c->last_total_bytes += size;
         u64 nmax = 0;
         int failed = -1;
         for (int p = 0; p < c->nranks; ++p) {
@@ -401,12 +506,14 @@ int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c) {
             return local_rc ? local_rc : gcc_set_err(GCC_E_INTERNAL, "group merge: rank %d failed (its error is on that rank)", failed);
         if (nmax <= cap) {
             if (4 * nmax < cap && cap > 1024) c->cap_others = std::max<u64>({1024, 3 * nmax / 2, cap / 2});
+            if (!local_rc) local_rc = gcc_forest_delta_arm(h);  // every rank holds the same partition: the next delta's base
             return local_rc ? own_error(c, local_rc) : GCC_OK;  // the peers finish: an error here is this rank's own
         }
         c->cap_others = std::max<u64>(3 * nmax / 2, 2 * cap);  // some list did not fit: again, larger
     }
     ++c->last_rounds;
     c->last_labels = true;
+    c->last_kind = 1;
     return merge_labels_rccl(h, c, V, st, local_rc);
 }
 
@@ -509,6 +616,43 @@ int gcc_group_merge(gcc_forest** hs, int n, gcc_comm** comms) {
         }
     } evs{ev};
     for (int i = 0; i < n; ++i) HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    // the delta round first (as gcc_forest_group_merge): every forest's delta into one buffer; if all are usable and
+    // fit, each forest absorbs the others' and arms again; otherwise the compact rounds, after which every forest arms
+    const char* de = getenv("GELLY_GROUP_DELTA");
+    for (u64 dcap = 1024; !(de && *de == '0');) {
+        const u64 size = round16(gcc_delta_msg_bytes(dcap));
+        if (size >= std::min<u64>(gcc_msg_bytes(V[0], std::max<u64>(1024, V[0] / 64)), 4ull * V[0])) break;
+        ABI_TRY(ensure(buf.d, buf.bytes, (u64)n * size));
+        for (int i = 0; i < n; ++i) {
+            ABI_TRY(gcc_forest_encode_delta(hs[i], static_cast<char*>(buf.d) + (u64)i * size, dcap));
+            HIP_TRY(hipEventRecord(ev[i], st[i]));
+        }
+        HIP_TRY(hipStreamWaitEvent(st[0], ev[n - 1], 0));
+        for (int j = 0; j < n - 1; ++j) HIP_TRY(hipStreamWaitEvent(st[0], ev[j], 0));
+        HIP_TRY(hipMemcpy2DAsync(buf.hdr, 16, buf.d, (size_t)size, 16, (size_t)n, hipMemcpyDeviceToHost, st[0]));
+        HIP_TRY(hipStreamSynchronize(st[0]));
+        u64 nmax = 0;
+        bool usable = true;
+        for (int p = 0; p < n; ++p) {
+            usable &= buf.hdr[4 * p + 3] == 0 && buf.hdr[4 * p + 2] == V[0];
+            nmax = std::max<u64>(nmax, buf.hdr[4 * p + 1]);
+        }
+        if (!usable) break;
+        if (nmax > dcap) {  // again, large enough
+            dcap = nmax;
+            continue;
+        }
+        for (int i = 0; i < n; ++i) {
+            for (int j = 0; j < n; ++j) HIP_TRY(hipStreamWaitEvent(st[i], ev[j], 0));  // every message written
+            ABI_TRY(gcc_forest_absorb_delta_many(hs[i], buf.d, size, (u32)n, (u32)i, dcap));
+        }
+        for (int i = 0; i < n; ++i) HIP_TRY(hipStreamSynchronize(st[i]));  // no later encode overwrites a message early
+        for (int i = 0; i < n; ++i) {
+            ABI_TRY(gcc_forest_delta_arm(hs[i]));
+            ABI_TRY(gcc_forest_compress(hs[i]));
+        }
+        return GCC_OK;
+    }
     u64 cap = std::max<u64>(1024, V[0] / 64);
     while (true) {
         const u64 size = round16(gcc_msg_bytes(V[0], cap));
@@ -517,6 +661,7 @@ int gcc_group_merge(gcc_forest** hs, int n, gcc_comm** comms) {
             ABI_TRY(gcc_forest_compress(hs[0]));
             for (int i = 1; i < n; ++i) ABI_TRY(gcc_forest_merge(hs[i], hs[0]));
             for (int i = 0; i < n; ++i) ABI_TRY(gcc_forest_sync(hs[i]));
+            for (int i = 0; i < n; ++i) ABI_TRY(gcc_forest_delta_arm(hs[i]));
             return GCC_OK;
         }
         ABI_TRY(ensure(buf.d, buf.bytes, (u64)n * size));
@@ -533,7 +678,10 @@ int gcc_group_merge(gcc_forest** hs, int n, gcc_comm** comms) {
         for (int i = 0; i < n; ++i) HIP_TRY(hipStreamSynchronize(st[i]));  // also: no encode overwrites a message early
         u64 nmax = 0;
         for (int p = 0; p < n; ++p) nmax = std::max<u64>(nmax, buf.hdr[4 * p + 1]);
-        if (nmax <= cap) return GCC_OK;
+        if (nmax <= cap) {
+            for (int i = 0; i < n; ++i) ABI_TRY(gcc_forest_delta_arm(hs[i]));
+            return GCC_OK;
+        }
         cap = std::max<u64>(3 * nmax / 2, 2 * cap);
     }
 }

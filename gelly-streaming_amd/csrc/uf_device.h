@@ -209,6 +209,36 @@ struct PipeRec {
     UF_HD void born(u32 x) const { aor(&touched[2 * (x >> 5) + 1], 1u << (x & 31)); }
 };
 
+// The delta merge's recorder (round 6; gelly_cc.hip fold_kernel<.., DELTA>, gcc_forest_encode_delta): every id whose
+// slot one of this fold's memory-side atomics changed — a root hooked (mark) or an id that left UNSEEN (born) — is
+// noted in the lane's event buffer; the fold kernel appends each wave's events to the forest's delta lists after the
+// unite. Those ids are the whole difference between the forest and the partition it held when the delta was armed:
+// that partition plus {(x, root(x))} for the noted x is the forest's partition. A unite notes at most
+// 3 (born lo, born hi, mark hi); kLaneEvents slots, a lane past them flags the delta as unusable.
+constexpr u32 kLaneEvents = 4;
+struct LaneEvents {
+    u32 x[kLaneEvents];
+    u32 n = 0;
+    UF_HD void note(u32 v) {
+        if (n < kLaneEvents) x[n] = v;
+        ++n;
+    }
+};
+struct DeltaRec {
+    LaneEvents* ev;
+    UF_HD void mark(u32 x) const { ev->note(x); }
+    UF_HD void born(u32 x) const { ev->note(x); }
+};
+struct BloomDeltaRec {  // both recorders: the incremental compress's bloom and the delta
+    u32* bloom;
+    LaneEvents* ev;
+    UF_HD void mark(u32 x) const {
+        aor(&bloom[bloom_word(x)], bloom_mask(x));
+        ev->note(x);
+    }
+    UF_HD void born(u32 x) const { ev->note(x); }
+};
+
 template <class L, bool SPLIT, class C = NoCount>
 struct UnionFind {
     // makeSet-on-first-sight (DisjointSet.union :99-104): an observed parent of v that is not UNSEEN

@@ -101,8 +101,11 @@ class RcclComm:
 
         rounds, labels, cap = ctypes.c_int(), ctypes.c_int(), ctypes.c_uint64()
         call("gcc_comm_last_merge", self._h, ctypes.byref(rounds), ctypes.byref(labels), ctypes.byref(cap))
+        kind, total, dcap = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint64()
+        call("gcc_comm_last_merge_kind", self._h, ctypes.byref(kind), ctypes.byref(total), ctypes.byref(dcap))
         return {"rounds": rounds.value, "labels": bool(labels.value), "bytes": self.last_bytes(),
-                "cap_others": cap.value}
+                "cap_others": cap.value, "kind": ("compact", "labels", "delta")[kind.value],
+                "bytes_all_rounds": total.value, "cap_delta": dcap.value}
 
     def close(self) -> None:
         from .native import call

@@ -72,6 +72,7 @@ _SIGS = {
     "gcc_comm_destroy": (c_int, [c_void_p]),
     "gcc_comm_info": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_uint64)]),
     "gcc_comm_last_merge": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_uint64)]),
+    "gcc_comm_last_merge_kind": (c_int, [c_void_p, POINTER(c_int), POINTER(c_uint64), POINTER(c_uint64)]),
     "gcc_forest_group_merge": (c_int, [c_void_p, c_void_p]),
     "gcc_group_merge": (c_int, [c_void_p, c_int, c_void_p]),
     "gcc_forest_device_ptr": (c_int, [c_void_p, POINTER(c_void_p)]),
@@ -110,6 +111,10 @@ _SIGS = {
     "gcc_forest_encode": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_forest_absorb": (c_int, [c_void_p, c_void_p, c_uint64]),
     "gcc_forest_absorb_many": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_uint64]),
+    "gcc_delta_msg_bytes": (c_uint64, [c_uint64]),
+    "gcc_forest_delta_arm": (c_int, [c_void_p]),
+    "gcc_forest_encode_delta": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "gcc_forest_absorb_delta_many": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_uint64]),
     # id dictionary for Java Long vertex ids (host-only)
     "gcc_idmap_create": (c_int, [c_uint32, POINTER(c_void_p)]),
     "gcc_idmap_destroy": (c_int, [c_void_p]),

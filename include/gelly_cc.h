@@ -150,6 +150,30 @@ int gcc_forest_absorb(gcc_forest* h, const void* d_msg, uint64_t cap_others);
 int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride_bytes, uint32_t count, uint32_t skip,
                            uint64_t cap_others);
 
+/* ---- the DELTA merge message (round 6): only what a forest changed since the last merge, shaped like the reference's
+ * per-window partials (…/SummaryBulkAggregation.java:80 folds each window into a fresh partial, so the all-window
+ * reduce moves only that window's unions, :81-83). After a group merge every rank holds the same partition P; the
+ * rank arms its delta (gcc_forest_delta_arm) and its next plain folds list every id whose slot they change (a root
+ * hooked, an id seen for the first time). The forest's partition is then P ∪ {(x, root(x)) : x listed}: at most 2
+ * pairs per edge folded, 8 B each, instead of the forest. Any other mutation (a filtered / seeded / bucketed fold, a
+ * merge, a reset, a device-pointer write) disarms it.
+ * Layout (one device buffer, gcc_delta_msg_bytes(cap_pairs) bytes):
+ *   u32 header[4] = { edges folded since arming, n_pairs, id_capacity, status }
+ *                   status 0; GCC_MSG_STATUS_FAILED (as above); GCC_DELTA_STATUS_UNARMED: the sender's changes were not
+ *                   all listed; GCC_DELTA_STATUS_OVERFLOW: its lists overflowed — either way the merge needs the compact
+ *                   message. n_pairs is the true count even past cap_pairs (only cap_pairs written: send again larger)
+ *   u32 pairs[2 * cap_pairs]            (x, root(x)) */
+#define GCC_DELTA_STATUS_UNARMED 2u
+#define GCC_DELTA_STATUS_OVERFLOW 3u
+uint64_t gcc_delta_msg_bytes(uint64_t cap_pairs);
+/* the forest's current partition becomes the base of its delta (after a merge every rank holds the same one) */
+int gcc_forest_delta_arm(gcc_forest* h);
+int gcc_forest_encode_delta(gcc_forest* h, void* d_msg, uint64_t cap_pairs); /* async on h's stream */
+/* h := h ∪ the partition of each of `count` delta messages at d_msgs + i * stride_bytes (i != skip), async; a message
+ * whose status is not 0 or whose id_capacity differs is ignored. Leaves the delta disarmed (the caller arms it). */
+int gcc_forest_absorb_delta_many(gcc_forest* h, const void* d_msgs, uint64_t stride_bytes, uint32_t count, uint32_t skip,
+                                 uint64_t cap_pairs);
+
 /* ---- cross-GPU group merge (gelly_group.cpp): replaces timeWindowAll(t).reduce(CombineCC) + the parallelism-1
  * Merger (…/SummaryBulkAggregation.java:81-83, …/SummaryAggregation.java:107-119). One communicator per GPU over
  * RCCL (xGMI); every rank's forest becomes the union of all ranks' forests — ONE all_gather of the compact messages
@@ -168,8 +192,13 @@ int gcc_comm_info(gcc_comm* c, int* nranks, int* rank, uint64_t* last_bytes);
 /* the last gcc_forest_group_merge: its all_gathers (compact rounds, + 1 for the label exchange), whether it ended with
  * the label exchange, and the speculative list capacity the next merge starts from (any may be NULL) */
 int gcc_comm_last_merge(gcc_comm* c, int* rounds, int* labels, uint64_t* cap_others);
+/* the last merge's kind (0 compact message, 1 label exchange, 2 delta), the bytes each rank contributed over all of its
+ * all_gathers (a failed delta round included) and the delta capacity (pairs) the next merge starts from */
+int gcc_comm_last_merge_kind(gcc_comm* c, int* kind, uint64_t* bytes_per_rank, uint64_t* cap_delta);
 /* collective over the communicator's ranks (every rank calls it with its forest, same id_capacity); synchronises
- * the forest's stream. Afterwards every rank's forest holds the global partition, compressed. */
+ * the forest's stream. Afterwards every rank's forest holds the global partition (compressed, unless the forest's
+ * lazy emission defers it: tune key emit_every) and its delta is armed. Round 6: the delta messages first (above), the
+ * compact rounds when a rank's delta is unusable or too large (GELLY_GROUP_DELTA=0: compact rounds only). */
 int gcc_forest_group_merge(gcc_forest* h, gcc_comm* c);
 /* single process: hs[0..n) := their union. Forests on one device need no comms (NULL); forests on several devices
  * need comms[i] = rank i of a gcc_comm_init_all group on hs[i]'s device. Synchronises every forest's stream. */
@@ -316,7 +345,12 @@ int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, 
  * inc_min_ids, inc_div, inc_inplace, inc_check, post_check, inc_split, fold_release, experimental, refresh_labels, bucket,
  * bucket_min_batch, bucket_min_ids, bucket_levels, bucket_sample, bucket_sample_sparse, bucket_hub_sample, bucket_p1, bucket_p2_per, bucket_p2_vw,
  * bucket_chunk, bucket_windows, bucket_items, bucket_items_p3,
- * bucket_slow2, bucket_defer, bucket_defer_c, compress_split, fold_split, inc_pipe, pin_chunk, lds_edges_per_word. Unknown keys return
+ * bucket_slow2, bucket_defer, bucket_defer_c, compress_split, fold_split, inc_pipe, emit_div, emit_rec, pin_chunk, lds_edges_per_word.
+ * emit_div (round 6): the lazy emission — in the plain regime (no tracked giant) gcc_forest_compress compresses only
+ * once the edges folded since the last compress reach id_capacity / emit_div (0: every emission compresses); the
+ * forest it leaves is the emitted summary (exact for find: every root is its component's minimum id), and every read
+ * (labels, find, size, digest, serialize, a merge message) compresses first. emit_rec: the folds between lazy emissions
+ * record for an incremental compress (1) or split paths (0). Unknown keys return
  * GCC_E_INVALID. One more key is a test hook, not a speed knob: fail_absorb = n makes the n-th next absorb fail with
  * GCC_E_INTERNAL before it launches anything (a rank's failure inside the cross-GPU group merge).
  * One setting is known to give wrong results and is refused (GCC_E_INVALID) unless `experimental` is set to 1 first:

@@ -29,6 +29,11 @@ struct gcc_forest {
     std::vector<u32> labels;  // canonical labels after compress (what gcc_forest_labels_device hands out)
     int fail_absorb = 0;
     bool bad_label = false;  // an out-of-range label was skipped (reported by the next sync, as on the device)
+    // the delta merge (round 6): while armed, the folds list every id whose slot they change (a hooked root, a new
+    // id), as the device fold's delta lists do; any other mutation disarms
+    bool armed = false;
+    std::vector<u32> delta;
+    u64 delta_edges = 0;
 };
 
 namespace {
@@ -45,12 +50,24 @@ u32 find(gcc_forest* h, u32 v) {
     return r;
 }
 
-void unite(gcc_forest* h, u32 a, u32 b) {
-    if (h->parent[a] == GCC_UNSEEN) h->parent[a] = a;  // makeSet on sight (DisjointSet.java:99-104)
-    if (h->parent[b] == GCC_UNSEEN) h->parent[b] = b;
+void unite(gcc_forest* h, u32 a, u32 b, bool record = false) {
+    std::vector<u32>* ev = record && h->armed ? &h->delta : nullptr;
+    if (!record) h->armed = false;
+    if (h->parent[a] == GCC_UNSEEN) {  // makeSet on sight (DisjointSet.java:99-104)
+        h->parent[a] = a;
+        if (ev) ev->push_back(a);
+    }
+    if (h->parent[b] == GCC_UNSEEN) {
+        h->parent[b] = b;
+        if (ev) ev->push_back(b);
+    }
     const u32 ra = find(h, a), rb = find(h, b);
-    if (ra < rb) h->parent[rb] = ra;
-    else if (rb < ra) h->parent[ra] = rb;
+    const u32 lo = ra < rb ? ra : rb, hi = ra < rb ? rb : ra;
+    if (lo != hi) {
+        h->parent[hi] = lo;
+        // a new id hung straight under the other's root is one event, as on the device (one CAS UNSEEN -> root)
+        if (ev && !(ev->size() && ev->back() == hi)) ev->push_back(hi);
+    }
 }
 
 void compress(gcc_forest* h) {
@@ -92,8 +109,9 @@ int gcc_forest_fold_host(gcc_forest* h, const uint32_t* pairs, uint64_t n) {
     CHECK_ARG(h && (pairs || !n), "null argument");
     for (u64 i = 0; i < n; ++i) {
         CHECK_ARG(pairs[2 * i] < h->cap && pairs[2 * i + 1] < h->cap, "id >= id_capacity");
-        unite(h, pairs[2 * i], pairs[2 * i + 1]);
+        unite(h, pairs[2 * i], pairs[2 * i + 1], true);
     }
+    h->delta_edges += n;
     return GCC_OK;
 }
 int gcc_forest_labels(gcc_forest* h, uint32_t* out, uint32_t n) {
@@ -138,6 +156,7 @@ int gcc_forest_labels_device(gcc_forest* h, const uint32_t** d) {
 }
 int gcc_forest_merge_labels_device(gcc_forest* into, const uint32_t* lab, uint32_t n) {
     CHECK_ARG(into && (lab || !n) && n <= into->cap, "bad argument");
+    into->armed = false;  // a mutation no delta list records (as on the device)
     std::vector<u32> copy(lab, lab + n);  // lab may be into's own label buffer
     for (u32 v = 0; v < n; ++v) {
         if (copy[v] == GCC_UNSEEN) continue;
@@ -196,6 +215,7 @@ int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride, u
     if (h->fail_absorb > 0 && --h->fail_absorb == 0)
         return gcc_set_err(GCC_E_INTERNAL, "gcc_forest_absorb_many: injected failure (tune key fail_absorb)");
     const u64 nw = ((u64)h->cap + 63) / 64;
+    h->armed = false;
     for (u32 p = 0; p < count; ++p) {
         if (p == skip) continue;
         const char* m = static_cast<const char*>(d_msgs) + (u64)p * stride;
@@ -216,6 +236,51 @@ int gcc_forest_absorb_many(gcc_forest* h, const void* d_msgs, uint64_t stride, u
             unite(h, oth[2 * i], oth[2 * i + 1]);
         }
     }
+    return GCC_OK;
+}
+uint64_t gcc_delta_msg_bytes(uint64_t cap_pairs) { return GCC_MSG_HEADER_BYTES + 8 * cap_pairs; }
+int gcc_forest_delta_arm(gcc_forest* h) {
+    CHECK_ARG(h, "null forest");
+    h->armed = true;
+    h->delta.clear();
+    h->delta_edges = 0;
+    return GCC_OK;
+}
+int gcc_forest_encode_delta(gcc_forest* h, void* d_msg, uint64_t cap_pairs) {
+    CHECK_ARG(h && d_msg, "null argument");
+    u32* hdr = static_cast<u32*>(d_msg);
+    u32* pairs = hdr + GCC_MSG_HEADER_BYTES / sizeof(u32);
+    hdr[0] = (u32)h->delta_edges;
+    hdr[1] = h->armed ? (u32)h->delta.size() : 0;
+    hdr[2] = h->cap;
+    hdr[3] = h->armed ? 0 : GCC_DELTA_STATUS_UNARMED;
+    if (h->armed)
+        for (u64 k = 0; k < h->delta.size() && k < cap_pairs; ++k) {
+            pairs[2 * k] = h->delta[k];
+            pairs[2 * k + 1] = find(h, h->delta[k]);
+        }
+    return GCC_OK;
+}
+int gcc_forest_absorb_delta_many(gcc_forest* h, const void* d_msgs, uint64_t stride, uint32_t count, uint32_t skip,
+                                 uint64_t cap_pairs) {
+    CHECK_ARG(h && (d_msgs || !count), "null argument");
+    CHECK_ARG(count <= 1 || stride >= gcc_delta_msg_bytes(cap_pairs), "stride smaller than a message");
+    if (h->fail_absorb > 0 && --h->fail_absorb == 0)
+        return gcc_set_err(GCC_E_INTERNAL, "gcc_forest_absorb_delta_many: injected failure (tune key fail_absorb)");
+    for (u32 p = 0; p < count; ++p) {
+        if (p == skip) continue;
+        const u32* hdr = reinterpret_cast<const u32*>(static_cast<const char*>(d_msgs) + (u64)p * stride);
+        if (hdr[2] != h->cap || hdr[3] != 0) continue;
+        const u32* pairs = hdr + GCC_MSG_HEADER_BYTES / sizeof(u32);
+        for (u64 k = 0; k < hdr[1] && k < cap_pairs; ++k) {
+            if (pairs[2 * k] >= h->cap || pairs[2 * k + 1] >= h->cap) {
+                h->bad_label = true;
+                continue;
+            }
+            unite(h, pairs[2 * k], pairs[2 * k + 1]);
+        }
+    }
+    h->armed = false;
     return GCC_OK;
 }
 int gcc_forest_tune(gcc_forest* h, const char* key, double value) {

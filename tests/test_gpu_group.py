@@ -195,13 +195,28 @@ def _spawn(world, fixture, env=None, timeout=240):
 
 def test_forest_group_c3_two_ranks_every_window():
     """C3 (G(n, m), 2^24 ids, 9.2M edges) split over 2 fresh ranks in 1M-edge windows, merged every
-    window by the production loop, every window of both ranks against the oracle's digests. C3 has no dominant
-    component: the compact rounds overflow their speculative capacity (repeat rounds) until the label exchange pays."""
+    window by the production loop, every window of both ranks against the oracle's digests. The first merge (nothing
+    armed yet) takes the compact rounds, which overflow their speculative capacity (a repeat round); every later one
+    the DELTA merge (round 6): at most 16 B per edge of the rank's window + the header, where rounds 4-5 all-gathered
+    64 MiB label arrays per rank (C3 has no dominant component)."""
     res = _spawn(2, "c3_gnm24/w1M")
     assert [r[:3] for r in res] == [(0, -1, "ok"), (1, -1, "ok")], res
     lasts = res[0][3]
-    assert any(x["rounds"] >= 2 and not x["labels"] for x in lasts), lasts  # a capacity repeat
-    assert any(x["labels"] for x in lasts), lasts                           # the label fallback
+    assert lasts[0]["kind"] == "compact" and lasts[0]["rounds"] >= 2, lasts[0]  # a capacity repeat
+    assert all(x["kind"] == "delta" for x in lasts[2:]), lasts
+    for x in lasts[2:]:
+        assert x["bytes"] <= 16 * (1 << 19) + 31, x  # 2^19 edges per rank per window
+
+
+def test_forest_group_c5_delta_every_window():
+    """C5 (2^24 ids, 256 windows of 2^16 edges: the short-window multi-GPU config) split over 2 fresh ranks: every
+    merge after the first is the delta merge, <= 16 B per edge of the rank's window (+ header), and every window of
+    both ranks matches the oracle's digests."""
+    res = _spawn(2, "c5_adversarial/w64K", timeout=300)
+    assert [r[:3] for r in res] == [(0, -1, "ok"), (1, -1, "ok")], res
+    lasts = res[0][3]
+    assert all(x["kind"] == "delta" and x["rounds"] == 1 for x in lasts[2:]), [x for x in lasts if x["kind"] != "delta"]
+    assert max(x["bytes"] for x in lasts[2:]) <= 16 * (1 << 15) + 31, max(x["bytes"] for x in lasts[2:])
 
 
 @pytest.mark.parametrize("at", [1, 2, 3])

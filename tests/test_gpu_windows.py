@@ -96,16 +96,21 @@ def test_c3_incremental_compress_every_window(torch_cuda, name):
     regime of round 2's stale label) and checked by the library itself (inc_check: every incremental
     compress against the roots of the forest it started from, every block's LDS bloom copy against memory), every
     window against the oracle."""
-    stats = fold_windows(torch_cuda, name, knobs={"incremental": 1, "inc_div": 8, "inc_check": 1})
+    stats = fold_windows(torch_cuda, name, knobs={"incremental": 1, "inc_div": 8, "inc_check": 1, **EAGER})
     checks, bad, lost = stats[0]
     assert checks >= 1 and bad == 0 and lost == 0, stats
 
 
+# the eager emission of rounds 1-5 (every emission compresses; the recording fold + in-place incremental compress): the
+# regime of the stale-label regression tests below. Round 6's default is the lazy emission (tune emit_div, tested below)
+EAGER = {"emit_div": 0}
+
+
 def test_c3_default_every_window(torch_cuda):
-    """C3 in 1M-edge windows at the DEFAULTS (incremental compress in place after the recording fold): the config of
+    """C3 in 1M-edge windows, eager emission (incremental compress in place after the recording fold): the config of
     round 3's recorded stale label. Every window against the oracle, and the post-compress check (a kernel after
     every incremental compress, nothing added before or inside it) at zero."""
-    stats = fold_windows(torch_cuda, "c3_gnm24/w1M", post=True)
+    stats = fold_windows(torch_cuda, "c3_gnm24/w1M", knobs=EAGER, post=True)
     checks, offenders, recs = stats[0]
     assert checks >= 8 and offenders == 0, stats
 
@@ -123,7 +128,7 @@ def test_c3_default_stress_no_stale_label(torch_cuda):
     offenders = checks = 0
     for s in range(60):
         ds = DisjointSet(V)
-        ds.tune(post_check=1)
+        ds.tune(post_check=1, **EAGER)
         for w in range(len(starts) - 1):
             ds.fold_device(d.data_ptr() + 8 * starts[w], starts[w + 1] - starts[w])
             ds.compress()
@@ -139,9 +144,9 @@ def test_c3_default_stress_no_stale_label(torch_cuda):
 
 
 def test_c5_default_every_window(torch_cuda):
-    """C5 (path + stars, 2^24 ids) in all 256 windows of 2^16 edges at the DEFAULTS (incremental compress), each
+    """C5 (path + stars, 2^24 ids) in all 256 windows of 2^16 edges, eager emission (incremental compress), each
     emission against the oracle, the post-compress check at zero."""
-    stats = fold_windows(torch_cuda, "c5_adversarial/w64K", post=True)
+    stats = fold_windows(torch_cuda, "c5_adversarial/w64K", knobs=EAGER, post=True)
     checks, offenders, recs = stats[0]
     assert checks >= 200 and offenders == 0, stats
 
@@ -149,7 +154,7 @@ def test_c5_default_every_window(torch_cuda):
 def test_c5_every_window(torch_cuda):
     """C5 (path + stars, 2^24 ids) in all 256 windows of 2^16 edges: 256 incremental compresses, each emission
     against the oracle."""
-    stats = fold_windows(torch_cuda, "c5_adversarial/w64K", knobs={"incremental": 1, "inc_check": 1})
+    stats = fold_windows(torch_cuda, "c5_adversarial/w64K", knobs={"incremental": 1, "inc_check": 1, **EAGER})
     checks, bad, lost = stats[0]
     assert checks >= 200 and bad == 0 and lost == 0, stats
 
@@ -182,3 +187,53 @@ def test_c4_split_8_group_merge(torch_cuda):
         ds.close()
     del d
     torch_cuda.cuda.empty_cache()
+
+
+def emitted_windows(torch_cuda, name, knobs=None, every=1):
+    """The LAZY emission (round 6 default, tune emit_div): per window a fold and an emission
+    (gcc_forest_compress), and the summary the emission left — the forest itself, not compressed unless the amortised
+    compress was due — against the oracle's digest. The check never compresses the forest under test: a second forest
+    on the device takes its partition (CombineCC = gcc_forest_merge reads parent pointers) and is digested. Returns how
+    many emissions found the forest uncompressed (so the lazy path, not a compress, is what was checked)."""
+    fx, starts = windows_of(name)
+    cfg = G.CONFIGS[fx["config"]]
+    E, V = cfg.info()
+    d = gen_device(torch_cuda, cfg)
+    ds, chk = DisjointSet(V), DisjointSet(V)
+    if knobs:
+        ds.tune(**knobs)
+    lazy = 0
+    for w in range(len(starts) - 1):
+        ds.fold_device(d.data_ptr() + 8 * starts[w], starts[w + 1] - starts[w])
+        ds.compress()
+        if w % every and w != len(starts) - 2:
+            continue
+        raw = ds.raw_parent()  # the emitted forest as it stands (no compress)
+        nonroot = (raw != 0xFFFFFFFF) & (raw != np.arange(V, dtype=np.uint32))
+        lazy += bool(np.any(raw[raw[nonroot]] != raw[nonroot]))  # some id two hops from its root: not compressed
+        chk.reset()
+        chk.merge(ds)
+        check_window(chk, fx, w, f"{name} lazy")
+    dig, seen, comps = ds.label_digest()  # and the labels a read materialises from it
+    want = fx["windows"][-1]
+    assert (str(dig), seen, comps) == (want["digest"], want["seen"], want["components"])
+    ds.close()
+    chk.close()
+    del d
+    torch_cuda.cuda.empty_cache()
+    return lazy
+
+
+@pytest.mark.parametrize("knobs", [None, {"emit_rec": 1}], ids=["split", "recording"])
+def test_c5_lazy_emission_every_window(torch_cuda, knobs):
+    """C5's 256 short windows at the default lazy emission (a compress per id_capacity / 8 folded edges): every
+    window's emitted summary exact, most of them uncompressed forests; with splitting folds + full compresses (default)
+    and with recording folds + incremental compresses (emit_rec = 1)."""
+    lazy = emitted_windows(torch_cuda, "c5_adversarial/w64K", knobs, every=4)
+    assert lazy >= 40, lazy
+
+
+def test_c3_lazy_emission_every_window(torch_cuda):
+    """C3 in 1M-edge windows at the default lazy emission: every window's emitted summary exact."""
+    lazy = emitted_windows(torch_cuda, "c3_gnm24/w1M")
+    assert lazy >= 2, lazy

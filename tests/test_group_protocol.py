@@ -94,6 +94,8 @@ def worker(rank, world, port, V, pairs, starts, want, q, env, uid=None):
             b, e = int(starts[w]), int(starts[w + 1])
             chunk = np.ascontiguousarray(pairs[b + (e - b) * rank // world: b + (e - b) * (rank + 1) // world])
             call("gcc_forest_fold_host", h, chunk.ctypes.data, len(chunk))
+            if env.get("DISARM_RANK") == str(rank) and env.get("DISARM_AT") == str(w):
+                call("gcc_forest_merge_labels_device", h, np.full(1, UNSEEN, np.uint32).ctypes.data, 1)  # disarms
             try:
                 group.merge_forest(f)
             except GellyCCError as ex:
@@ -203,6 +205,8 @@ def test_compact_rounds_every_window(world, torch_bootstrap):
     lasts = res[0][4]
     assert any(last["rounds"] >= 2 and not last["labels"] for last in lasts), lasts  # a repeat round ran
     assert not lasts[-1]["labels"]  # the compact form pays at the end
+    # armed after the first merge: the short windows take the delta, the last (long) one the smaller compact message
+    assert lasts[0]["kind"] == "compact" and any(last["kind"] == "delta" for last in lasts), lasts
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -250,3 +254,44 @@ def test_dead_peer_is_an_error_not_a_hang():
                            timeout=60)
     assert codes[1] == 3, codes
     assert len(res) == 1 and res[0][0] == 0 and res[0][2] == "error", res
+
+
+def short_windows_case(n_windows=24, w=2048):
+    """C5's shape at a CPU-test size: a shuffled path plus stars (gcc_gen ADVERSARIAL), many short windows."""
+    import oracle as orc
+    from gelly_stream import generators as G
+
+    cfg = G.scaled(G.CONFIGS["c5_adversarial"], scale=14, n_stars=16, star_size=1024)
+    pairs = G.generate_host(cfg)[: n_windows * w]
+    _, V = cfg.info()
+    starts = np.arange(0, len(pairs) + 1, w, dtype=np.uint64)
+    want = orc.cc_stream(pairs, starts, V, want_labels=True)["labels"]
+    return V, pairs, starts, want
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_delta_merge_every_window(world):
+    """The delta merge (round 6): after the first (compact) merge every rank is armed, and each later window moves only
+    (x, root(x)) for the ids the rank's fold changed — at most 2 per edge, 8 B each: the all_gather is <= 16 B per edge
+    of the largest rank's window + the header, once the capacity has followed the windows (it is twice the largest
+    window of the last merge). Every window of every rank equals the oracle's global partition."""
+    V, pairs, starts, want = short_windows_case()
+    res, _ = run_world(world, V, pairs, starts, want)
+    assert [r[:3] for r in res] == [(r, -1, "ok") for r in range(world)], res
+    for r in res:
+        lasts = r[4]
+        assert lasts[0]["kind"] == "compact", lasts[0]
+        assert all(last["kind"] == "delta" and last["rounds"] == 1 for last in lasts[2:]), lasts
+        per_rank = [int(starts[k + 1] - starts[k] + world - 1) // world for k in range(len(starts) - 1)]
+        for k, last in enumerate(lasts[2:], start=2):
+            assert last["bytes"] <= 16 * per_rank[k] + 16 + 15, (k, last)
+
+
+def test_delta_unarmed_rank_takes_the_compact_rounds():
+    """A rank whose window took an unrecorded mutation sends an UNARMED delta (host forest: a merge_labels call
+    disarms it): every rank then takes the compact rounds, exact, and is armed again after it."""
+    V, pairs, starts, want = short_windows_case(n_windows=6)
+    res, _ = run_world(2, V, pairs, starts, want, env={"DISARM_RANK": "1", "DISARM_AT": "3"})
+    assert [r[:3] for r in res] == [(0, -1, "ok"), (1, -1, "ok")], res
+    kinds = [last["kind"] for last in res[0][4]]
+    assert kinds[3] == "compact" and kinds[4] == "delta", kinds

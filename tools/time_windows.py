@@ -95,6 +95,7 @@ def main() -> int:
                 step(ds)
             ds.sync()
             times[v].append((time.perf_counter() - t0) / a.steps * 1e3)
+    chk = DisjointSet(V)
     for v in variants:
         ds = forests[v]
         bad = []
@@ -104,9 +105,11 @@ def main() -> int:
             ds.compress()  # the emission, lazy or not
             if "windows" not in fx and w < len(starts) - 2:
                 continue  # (fixed windows over a one-window fixture: the last one is checked)
-            # the emitted summary as it stands (the raw forest: no compress, so a lazy emission's state is what is
-            # checked), its roots found on the host
-            got, seen, comps = forest_digest(ds.raw_parent())
+            # the emitted summary as it stands: the raw forest (no compress of ds, so a lazy emission's state is what
+            # is checked) merged into a fresh forest on the device (CombineCC reads parent pointers), its digest there
+            chk.reset()
+            chk.merge(ds)
+            got, seen, comps = chk.label_digest()
             want = fx["windows"][w] if "windows" in fx else fx
             if (str(got), seen, comps) != (want["digest"], want["seen"], want["components"]):
                 bad.append(w)
