@@ -531,7 +531,10 @@ static int signed_fold_bucketed(gcc_signed* h, const u64* edges, u64 n, const u3
     const char* stats = std::getenv("GELLY_BUCKET_STATS");
     a.want_counts = stats && *stats && *stats != '0';
     int rc = gcc_internal_signed_bucket(h->bk_scratch, &a);
-    if (rc) return rc;
+    if (rc) {  // N2 must be zero before the next batch (sb_join clears it on the normal path): clear it here
+        (void)hipMemsetAsync(h->d_n2, 0, nw * sizeof(u32), h->stream);
+        return rc;
+    }
     std::memcpy(h->last_counts, a.counts, sizeof(a.counts));
     if (a.want_counts)
         std::fprintf(stderr, "[signed-bucket] n=%llu level 1: emitted %llu slow %llu; level 2: emitted %llu slow %llu; level 3: emitted %llu slow %llu\n",
@@ -561,7 +564,9 @@ static int signed_fold(gcc_signed* h, const u32* d_pairs, u64 n) {
     hipLaunchKernelGGL(signed_snapshot_kernel, dim3(grid_for_n(nw * 16, kMaxGrid)), dim3(256), 0, h->stream, h->d_word, h->cap,
                        vote, min_count, h->d_gbits);
     HIP_TRY(hipGetLastError());
-    if (n > s && h->bucket && n - s >= h->bucket_min && h->cap <= (1u << 28) &&
+    // id ranges up to 2^27 (past 2^27 the bucketing takes untested shapes — 6-B emit entries, 12K-edge P1
+    // tiles — so those ranges keep the giant-filtered fold)
+    if (n > s && h->bucket && n - s >= h->bucket_min && h->cap <= (1u << 27) &&
         ((reinterpret_cast<uintptr_t>(edges + s) & 15) == 0)) {
         u32 hv[2];  // the vote: a component to filter against, or the plain fold (no bucketing for it)
         HIP_TRY(hipMemcpyAsync(hv, vote, sizeof(hv), hipMemcpyDeviceToHost, h->stream));
@@ -834,6 +839,7 @@ int gcc_signed_words(gcc_signed* h, uint32_t* out, uint32_t n) {
         HIP_TRY(hipMemcpyAsync(h->host_words.data(), h->d_word, (size_t)h->cap * sizeof(u32), hipMemcpyDeviceToHost,
                                h->stream));
         HIP_TRY(hipStreamSynchronize(h->stream));
+        if ((rc = gcc_internal_take_err(h->bk_scratch, h->stream))) return rc;  // the bucketed fold's skipped ids
         h->host_valid = true;
     }
     std::memcpy(out, h->host_words.data(), (size_t)n * sizeof(u32));
@@ -847,7 +853,7 @@ int gcc_signed_success(gcc_signed* h, int* success) {
     HIP_TRY(hipMemcpyAsync(&f, h->d_fail, sizeof(u32), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     *success = f ? 0 : 1;
-    return GCC_OK;
+    return gcc_internal_take_err(h->bk_scratch, h->stream);  // the bucketed fold's skipped ids
 }
 
 int gcc_signed_capacity(gcc_signed* h, uint32_t* id_capacity) {

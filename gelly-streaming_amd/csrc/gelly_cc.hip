@@ -3544,8 +3544,25 @@ static int bucketize(gcc_forest* f, const u64* edges, u64 n, u32** lo_out, bk::u
 // rest, the closing compress into a->out. No host synchronisation: the lists' lengths and per-slice counts stay on
 // the device (ctr[1], ctr[2]; a->hist), and their P1 layouts take them from there (round 5: one sync per list and a
 // sampled layout each cost 0.3 ms of the share's 4.65).
+int gcc_internal_take_err(gcc_forest* f, hipStream_t stream) {
+    if (!f) return GCC_OK;
+    DeviceGuard g(f->device);
+    const hipStream_t own = f->stream;
+    f->stream = stream;
+    const int rc = stream_sync_checked(f);
+    f->stream = own;
+    return rc;
+}
+
 int gcc_internal_signed_bucket(gcc_forest* f, GccSignedBucketArgs* a) {
     DeviceGuard g(f->device);
+    // the scratch runs on the signed handle's stream for this fold only: its own stream is restored on every return
+    // (gcc_forest_destroy synchronises f->stream, which must not be a stream the signed handle may have destroyed since)
+    struct StreamRestore {
+        gcc_forest* f;
+        hipStream_t own;
+        ~StreamRestore() { f->stream = own; }
+    } restore{f, f->stream};
     f->stream = a->stream;
     const u32 ns = bucket_slices(f);
     const u32 nw16 = (u32)(((u64)a->cap + 15) / 16);

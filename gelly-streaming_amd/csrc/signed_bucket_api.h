@@ -29,5 +29,9 @@ struct GccSignedBucketArgs {
     uint64_t counts[6];     // out: emitted and slow entries of levels 1-3 (diagnostics)
 };
 
-// gcc status; `scratch` = a CC forest of the same id range, used for its bucket storage only (gcc_forest_create)
+// gcc status; `scratch` = a CC forest of the same id range, used for its bucket storage only (gcc_forest_create).
+// Runs on a->stream; the scratch forest's own stream is restored before it returns.
 int gcc_internal_signed_bucket(gcc_forest* scratch, GccSignedBucketArgs* a);
+// The device error word the bucketed fold's kernels set (an id >= id_capacity skipped, or an internal list entry out
+// of range), read on `stream` (synchronises it) and cleared: GCC_OK, or the error the signed handle reports.
+int gcc_internal_take_err(gcc_forest* scratch, hipStream_t stream);

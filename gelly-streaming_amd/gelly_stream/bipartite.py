@@ -153,7 +153,7 @@ class Candidates:
 
     def tune(self, **knobs) -> "Candidates":
         """Speed-only knobs of the signed fold (gcc_signed_tune): giant, sample_shift, min_share, unroll, xcd, xcd_min,
-        bucket, bucket_min, bucket_levels."""
+        bucket (the bucketed fold: id ranges up to 2^27), bucket_min, bucket_levels, bucket_items."""
         for k, v in knobs.items():
             call("gcc_signed_tune", self.handle, k.encode(), float(v))
         return self

@@ -232,9 +232,12 @@ int gcc_signed_device_words(gcc_signed* h, const uint32_t** d_words);
  * share of sampled edges below which the batch takes the plain fold), "unroll" (1/2/4/8 edges per lane per step of
  * the giant-filtered fold), "xcd" (1/0: that fold over the batch split into 8 parts by source id, one part per XCD)
  * and "xcd_min" (the edges past the sample from which the split is used), "bucket" (1/0: that fold bucketed by the
- * ids' 2^19-id slices, both snapshot lookups in LDS — round 5, the default for id ranges up to 2^26; one host
- * synchronisation per batch, for the vote), "bucket_min" (the edges past the sample from which it is used), "bucket_levels" (1, 2 or 3 filter levels
- * before the rest), "bucket_items" (work items per CU of its filter / check kernels; 2). GCC_E_INVALID for an unknown key. */
+ * ids' 2^19-id slices, both snapshot lookups in LDS — round 5, the default for id ranges up to 2^27; one host
+ * synchronisation per batch, for the vote; it keeps a scratch CC forest (8 B per id) and three lists of 8 B per edge
+ * of the largest batch for the handle's lifetime), "bucket_min" (the edges past the sample from which it is used),
+ * "bucket_levels" (1, 2 or 3 filter levels before the rest), "bucket_items" (work items per CU of its filter / check
+ * kernels; 2). An id >= id_capacity in a bucketed batch is skipped and reported (GCC_E_INVALID) by the next
+ * gcc_signed_words / gcc_signed_success. GCC_E_INVALID for an unknown key. */
 int gcc_signed_tune(gcc_signed* h, const char* key, double value);
 /* the emission on the device: the canonical words replace the forest (asynchronous on the forest's stream; what
  * gcc_signed_words copies out). After a failure the words are unspecified (the emitted value is (false, {})). */

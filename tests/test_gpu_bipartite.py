@@ -267,6 +267,38 @@ def test_bucketed_fold_many_slices(odd, knobs):
     c.close()
 
 
+@pytest.mark.parametrize("extra_ids", [0, 1 << 20])
+def test_bucketed_fold_largest_default_id_range(extra_ids):
+    """the bucketed signed fold is the default up to 2^27 ids (256 slices: the largest shape it takes by
+    default, 4-B key-only emit lists); past 2^27 the giant-filtered fold runs. A kron stream over 2^27 ids (+ 2^20
+    unused ids above it) mapped bipartite, 2^25 edges: the same words and success as bucket = 0, with and without an
+    odd edge between two hubs' sides."""
+    import torch
+
+    cfg = G.scaled(G.CONFIGS["c4_kron26"], scale=27, n_edges=1 << 25)
+    E, V0 = cfg.info()
+    V = V0 + extra_ids
+    d = torch.empty(2 * E, dtype=torch.int32, device="cuda:0")
+    G.generate_device(cfg, 0, E, d.data_ptr(), 0)
+    G.to_bipartite_device(d)
+    for odd in (False, True):
+        if odd:  # one edge between two even ids (the same side): an odd cycle once both sides are connected
+            d[E] = d[0]
+            d[E + 1] = d[2]
+        ref = Candidates(V).tune(bucket=0)
+        ref.fold_device(d.data_ptr(), E)
+        c = Candidates(V)
+        c.fold_device(d.data_ptr(), E)
+        assert c.getSuccess() == ref.getSuccess()
+        if not odd:
+            assert ref.getSuccess()
+            assert np.array_equal(c.words(), ref.words())
+        ref.close()
+        c.close()
+    del d
+    torch.cuda.empty_cache()
+
+
 def test_giant_fold_knobs_and_no_dominant_component():
     """The giant-filtered fold's knobs change speed only: to_bipartite(scaled C3) (no dominant component: the
     snapshot stays empty) and a kron stream (a sample of 1/2 or 1/1024, min_share 1.0 = never filter) fold to the
