@@ -586,6 +586,13 @@ def config_legs(local, steps, warmup, digests, tune, d_edges=None):
                                           "C4's first 2^27 edges into a fresh summary: what each rank folds at N = 8")
         except Exception as e:
             out["c4_share"] = {"error": repr(e)}
+        for key, n in (("c4_quarter", 1 << 28), ("c4_half", 1 << 29)):  # the per-rank folds at N = 4 and 2
+            try:
+                out[key] = windows_leg(key, factory(V4), [(base, n)], max(2, steps // 2), 1, digests.get(key), V4, key,
+                                       f"C4's first 2^{n.bit_length() - 1} edges into a fresh summary: what each rank "
+                                       f"folds at N = {E4 // n} (DESIGN.md §6's predicted curve)")
+            except Exception as e:
+                out[key] = {"error": repr(e)}
         try:
             w = 1 << 27
             out["c4_kron26/w8"] = windows_leg("c4_kron26/w8", factory(V4), wins(base, list(range(0, E4 + 1, w))),

@@ -2228,6 +2228,10 @@ struct gcc_forest {
     u32* d_giant = nullptr;  // [0], [1]: tracked-component root slots; [4], [5]: the vote's share (giant_vote_kernel)
     bool filter_off = false;  // the vote found no giant: this forest folds without the filter until reset
     bool has_giant = false;
+    // a compress (not a fold's sample) elected the tracked component: its share was not checked yet (round 6: a short
+    // first window, e.g. C5's 2^15-edge chunks at N = 2, went straight to the filtered regime over a component of a few
+    // ids, and the filtered fold keeps no delta lists). launch_fold reads the share once and decides filter_off
+    bool share_unchecked = false;
     int giant_slot = 0;  // d_giant[giant_slot] = root of the tracked component as of the last refresh
     u32* d_qcount = nullptr;  // per-block slow-edge counts of the last filtered launch (measurement)
     // fused seeding: dedicated flag bytes (one per id, rounded up to a bitmap word), marked with an epoch
@@ -2687,9 +2691,11 @@ static int compress_now(gcc_forest* h, const char* name = "compress", u64* oth =
             HIP_TRY(hipMemsetAsync(h->d_bloom, 0, 2 * (size_t)(gcc::kBloomBits / 8), h->stream));
             h->rec_all = false;
         }
-        if (!h->has_giant)  // first refresh of this forest: elect the component to track
+        if (!h->has_giant) {  // first refresh of this forest: elect the component to track
             rc = launch_k(h, "vote", 0, giant_vote_kernel, dim3(1), dim3(1024), 0, h->d_parent, h->cap,
                           h->d_giant + h->giant_slot, h->d_giant + 4);
+            h->share_unchecked = true;  // the next fold checks the vote's share (launch_fold)
+        }
         u32* clear = h->d_bloom ? h->bloom(h->bloom_cur ^ 1) : nullptr;
         if (!rc && inc_here && h->rec_all) {
             const char* kname = std::strcmp(name, "refresh") ? "compress_inc" : "refresh_inc";
@@ -2751,9 +2757,11 @@ static int refresh_now(gcc_forest* h) {
     int rc = pipe_exit(h);
     if (!rc) rc = alloc_filter(h);
     if (rc) return rc;
-    if (!h->has_giant)
+    if (!h->has_giant) {
         rc = launch_k(h, "vote", 0, giant_vote_kernel, dim3(1), dim3(1024), 0, h->d_parent, h->cap,
                       h->d_giant + h->giant_slot, h->d_giant + 4);
+        h->share_unchecked = true;
+    }
     if (!rc)
         rc = launch_k(h, "refresh_bits", 0, compress_bits_kernel<true>, dim3(chunk_grid(h->cap, kBitsU, kBlock, kMaxGrid)),
                       dim3(kBlock), 0, h->d_parent, (u32*)nullptr, h->cap, (const u32*)(h->d_giant + h->giant_slot),
@@ -3346,6 +3354,15 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
             if (masks) h->mask_version = h->version;
         }
         return GCC_OK;
+    }
+    if (h->share_unchecked && !h->pending_reset) {
+        h->share_unchecked = false;
+        if (h->has_giant && !h->filter_off && h->filter_enabled() && t.filter_min_share > 0 && h->d_giant) {
+            u32 share[2] = {0, 0};  // once per forest
+            HIP_TRY(hipMemcpyAsync(share, h->d_giant + 4, sizeof(share), hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(hipStreamSynchronize(h->stream));
+            h->filter_off = share[0] < t.filter_min_share * share[1];
+        }
     }
     if (seeded) {
         rc = launch_seed(h, d_pairs, n);
@@ -4006,6 +4023,7 @@ int gcc_forest_reset(gcc_forest* h) {
     h->compressed = true;  // all UNSEEN is canonical
     h->has_giant = false;  // the giant bitmap described the old forest
     h->filter_off = false;
+    h->share_unchecked = false;
     h->edges_since_compress = 0;
     h->delta_armed = false;
     return GCC_OK;

@@ -56,6 +56,10 @@ CONFIGS = {
     # C4's per-GPU share: the first 2^27 edges of the C4 stream (same seed, counter-based generator), all 2^26
     # ids. Weak-scaled over W ranks (bench.py) it is the first W * 2^27 edges: W = 8 is exactly C4.
     "c4_share": StreamConfig("c4_share", native.GCC_GEN_RMAT, scale=26, n_edges=2 << 26, seed=SEED_BASE | 4),
+    # C4's per-rank folds at N = 4 and N = 2 (the first 2^28 / 2^29 edges): the measured inputs of DESIGN.md §6's
+    # predicted 1/2/4/8 curve (bench.py config legs, round 6)
+    "c4_quarter": StreamConfig("c4_quarter", native.GCC_GEN_RMAT, scale=26, n_edges=4 << 26, seed=SEED_BASE | 4),
+    "c4_half": StreamConfig("c4_half", native.GCC_GEN_RMAT, scale=26, n_edges=8 << 26, seed=SEED_BASE | 4),
     # C5: adversarial path over 2^23 ids + 1024 stars of 8192 ids, windows of 2^16 edges
     "c5_adversarial": StreamConfig("c5_adversarial", native.GCC_GEN_ADVERSARIAL, scale=23, n_stars=1024,
                                    star_size=8192, seed=SEED_BASE | 5, window_edges=1 << 16),

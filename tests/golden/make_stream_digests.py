@@ -30,7 +30,7 @@ C2_BATCHES = 4
 
 
 def entries():
-    names = ["c2_rmat20", "c3_gnm24", "c5_adversarial", "c4_share", "c4_kron26"]
+    names = ["c2_rmat20", "c3_gnm24", "c5_adversarial", "c4_share", "c4_quarter", "c4_half", "c4_kron26"]
     names += [f"c2_rmat20@{k}" for k in range(1, C2_BATCHES)]
     names += list(WINDOWED)
     return names

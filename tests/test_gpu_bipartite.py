@@ -285,6 +285,7 @@ def test_bucketed_fold_largest_default_id_range(extra_ids):
         if odd:  # one edge between two even ids (the same side): an odd cycle once both sides are connected
             d[E] = d[0]
             d[E + 1] = d[2]
+        torch.cuda.synchronize()  # the summaries fold on their own non-blocking streams
         ref = Candidates(V).tune(bucket=0)
         ref.fold_device(d.data_ptr(), E)
         c = Candidates(V)
