@@ -2204,6 +2204,10 @@ struct FoldTune {
     // the plain folds between lazy emissions: record their mutations for an incremental compress (1) or split paths
     // and leave the compress that follows full (0: measured faster at C5's 32 windows per compress)
     int emit_rec = 0;
+    // the giant-filtered regime's lazy emission (A/B, round 6): the emission refreshes only the tracked component's
+    // bitmap (compress_bits_kernel without labels: 4 B per id read instead of 4 read + 4 written), and the labels
+    // wait for a read (1); or it compresses (0)
+    int emit_filtered = 0;
 };
 constexpr u32 kFilterMinIds = 1u << 16;  // forests over fewer ids never use the filter
 
@@ -4561,6 +4565,10 @@ int gcc_forest_compress(gcc_forest* h) {
     if (h->tune.emit_div > 0 && !h->pipe && !h->compressed && (!h->filter_enabled() || h->filter_off) &&
         h->edges_since_compress * (u64)h->tune.emit_div < (u64)h->cap)
         return flush_fold(h);
+    if (h->tune.emit_filtered && !h->pipe && !h->compressed && h->filter_enabled() && !h->filter_off && h->has_giant) {
+        int rc = flush_fold(h);
+        return rc ? rc : refresh_now(h);
+    }
     return compress_async(h, false);
 }
 
@@ -4680,6 +4688,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "inc_pipe") t.inc_pipe = std::max(0, std::min(2, (int)value));
     else if (k == "emit_div") t.emit_div = std::max(0, std::min(1 << 20, (int)value));
     else if (k == "emit_rec") t.emit_rec = value != 0;
+    else if (k == "emit_filtered") t.emit_filtered = value != 0;
     else if (k == "pin_chunk") t.pin_chunk = (u64)value;
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
