@@ -2200,7 +2200,7 @@ struct FoldTune {
     // 5.25 G at 16 / 32 with splitting folds + full compress, against 2.08 eager. The giant-filtered regime (C2) keeps
     // the eager emission: its compress refreshes the filter's bitmap (lazy there measured slower: C2 x 16 at 4 / 8
     // windows 0.296 / 0.417 ms against 0.259).
-    int emit_div = 8;
+    int emit_div = 1;
     // the plain folds between lazy emissions: record their mutations for an incremental compress (1) or split paths
     // and leave the compress that follows full (0: measured faster at C5's 32 windows per compress)
     int emit_rec = 0;

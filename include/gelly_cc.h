@@ -348,13 +348,14 @@ int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, 
  * inc_min_ids, inc_div, inc_inplace, inc_check, post_check, inc_split, fold_release, experimental, refresh_labels, bucket,
  * bucket_min_batch, bucket_min_ids, bucket_levels, bucket_sample, bucket_sample_sparse, bucket_hub_sample, bucket_p1, bucket_p2_per, bucket_p2_vw,
  * bucket_chunk, bucket_windows, bucket_items, bucket_items_p3,
- * bucket_slow2, bucket_defer, bucket_defer_c, compress_split, fold_split, inc_pipe, emit_div, emit_rec, pin_chunk, lds_edges_per_word.
+ * bucket_slow2, bucket_defer, bucket_defer_c, compress_split, fold_split, inc_pipe, emit_div, emit_rec, emit_filtered,
+ * pin_chunk, lds_edges_per_word. Unknown keys return GCC_E_INVALID.
  * emit_div (round 6): the lazy emission — in the plain regime (no tracked giant) gcc_forest_compress compresses only
- * once the edges folded since the last compress reach id_capacity / emit_div (0: every emission compresses); the
- * forest it leaves is the emitted summary (exact for find: every root is its component's minimum id), and every read
- * (labels, find, size, digest, serialize, a merge message) compresses first. emit_rec: the folds between lazy emissions
- * record for an incremental compress (1) or split paths (0). Unknown keys return
- * GCC_E_INVALID. One more key is a test hook, not a speed knob: fail_absorb = n makes the n-th next absorb fail with
+ * once the edges folded since the last compress reach id_capacity / emit_div (default 1; 0: every emission compresses);
+ * the forest it leaves is the emitted summary (exact for find: every root is its component's minimum id), and every
+ * read (labels, find, size, digest, serialize, a merge message) compresses first. emit_rec: the folds between lazy
+ * emissions record for an incremental compress (1) or split paths (0). emit_filtered: in the giant-filtered regime the
+ * emission refreshes only the tracked component's bitmap (1) or compresses (0). One more key is a test hook, not a speed knob: fail_absorb = n makes the n-th next absorb fail with
  * GCC_E_INTERNAL before it launches anything (a rank's failure inside the cross-GPU group merge).
  * One setting is known to give wrong results and is refused (GCC_E_INVALID) unless `experimental` is set to 1 first:
  * inc_split = 1 (path splitting in the recording fold before an in-place incremental compress: round 3's stale label,

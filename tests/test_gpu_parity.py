@@ -578,6 +578,10 @@ KNOB_CASES = {
     # inc_split = 1 is refused without `experimental` (test_unsafe_setting_needs_experimental); its default here
     "inc_split": {"incremental": 1, "inc_min_ids": 1024, "inc_split": 0},
     "experimental": {"experimental": 1},
+    # the lazy emission (round 6): eager, and a compress only per id_capacity folded edges in the plain regime
+    "emit_div": [{"emit_div": 0}, {"emit_div": 1, "filter": 0}],
+    "emit_rec": {"emit_rec": 1, "incremental": 1, "inc_min_ids": 1024, "filter": 0},
+    "emit_filtered": {"emit_filtered": 1},
 }
 
 
@@ -629,4 +633,5 @@ def test_every_tuning_knob_is_bit_exact(torch_cuda):
             for w in range(len(starts) - 1):
                 b, e = int(starts[w]), int(starts[w + 1])
                 ds.fold_device(d.data_ptr() + 8 * b, e - b)
+                ds.compress()  # the window's emission (lazy or not: the labels read below compress if it was)
                 assert orc.label_digest(ds.labels()) == int(want[w]), (key, w)
