@@ -256,9 +256,9 @@ def test_incremental_compress_windows(torch_cuda):
     want = orc.cc_stream(G.generate_host(cfg), starts, V, partitions=2, threads=2)
     d = device_stream(torch_cuda, cfg)
     inc, full, spare = DisjointSet(V), DisjointSet(V), DisjointSet(V)
-    inc.tune(incremental=1)  # opt-in since the end of round 3
+    inc.tune(incremental=1, emit_div=0)  # the eager emission's incremental compress (round 6's default emission is lazy)
     full.tune(incremental=0)
-    spare.tune(incremental=1, inc_inplace=0)
+    spare.tune(incremental=1, inc_inplace=0, emit_div=0)
     side = DisjointSet(V)  # a partial forest merged into `inc` mid-stream (CombineCC)
     side.fold_device(d.data_ptr(), W)
     for w in range(len(starts) - 1):

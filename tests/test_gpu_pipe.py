@@ -71,7 +71,7 @@ def test_overlapped_stream_matches_oracle(torch_cuda, name):
     nw = len(starts) - 1
     sample = {3, 4, nw // 3, nw // 2 + 1, nw - 2} if nw > 8 else {2, 5}
     ds = DisjointSet(V)
-    ds.tune(inc_pipe=1)
+    ds.tune(inc_pipe=1, emit_div=0)
     ds.enable_timing(1)
     bad = []
     for rep in range(2):  # twice into the same forest (reset between): the roots arrays restart from UNSEEN
@@ -98,7 +98,7 @@ def test_c5_every_window_read(torch_cuda):
     E, V = cfg.info()
     d = gen_device(torch_cuda, cfg)
     ds = DisjointSet(V)
-    ds.tune(inc_pipe=1)
+    ds.tune(inc_pipe=1, emit_div=0)
     bad = []
     for w in range(len(starts) - 1):
         ds.fold_device(d.data_ptr() + 8 * starts[w], starts[w + 1] - starts[w])
@@ -124,8 +124,8 @@ def test_leaving_and_reentering_the_mode(torch_cuda):
     E, V = cfg.info()
     W = 1 << 16
     pipe, ref = DisjointSet(V), DisjointSet(V)
-    pipe.tune(inc_pipe=1)
-    ref.tune(inc_pipe=0)
+    pipe.tune(inc_pipe=1, emit_div=0)
+    ref.tune(inc_pipe=0, emit_div=0)
     side = DisjointSet(V)
     side.fold_device(d.data_ptr(), 3 * W)
     host = d[: 2 * W].cpu().numpy().view(np.uint32).reshape(-1, 2)
@@ -191,8 +191,8 @@ def test_partial_last_chunk(torch_cuda, V):
     starts = np.arange(0, len(pairs) + 1, W, dtype=np.uint64)
     want = orc.cc_stream(pairs, starts, V, partitions=1, threads=2)
     pipe, ref = DisjointSet(V), DisjointSet(V)
-    pipe.tune(inc_pipe=1)
-    ref.tune(inc_pipe=0)
+    pipe.tune(inc_pipe=1, emit_div=0)
+    ref.tune(inc_pipe=0, emit_div=0)
     pipe.enable_timing(1)
     for w in range(len(starts) - 1):
         for ds in (pipe, ref):
