@@ -54,6 +54,16 @@ KERNEL_BYTES = {
     "bucket_init_kernel": (4.125, "id"),    # parent write + 1 bitmap bit
 }
 C2_BATCHES = 4  # rotating C2 batches (tests/golden/stream_digests.json c2_rmat20@k)
+# DESIGN.md §6's predicted curve (round 6): per workload and N, the per-rank fold, the merge kernels, the message and the
+# modelled all_gather (ms; bytes per rank), so that a multi-GPU line can be read against its prediction
+PREDICTED = {
+    "c4_kron26": {1: {"fold_ms": 9.04, "ms_per_step": 9.04},
+                  2: {"fold_ms": 5.03, "merge_kernels_ms": 0.24, "message_bytes": 8.9e6, "all_gather_ms": 0.25, "ms_per_step": 5.52},
+                  4: {"fold_ms": 2.86, "merge_kernels_ms": 0.28, "message_bytes": 9.3e6, "all_gather_ms": 0.26, "ms_per_step": 3.40},
+                  8: {"fold_ms": 1.78, "merge_kernels_ms": 0.36, "message_bytes": 10.0e6, "all_gather_ms": 0.27, "ms_per_step": 2.41}},
+    "c5_adversarial": {n: {"ms_per_window": 0.06, "message_bytes_per_window": 16 * (1 << 16) // n + 16, "ms_per_step": 15.0}
+                       for n in (2, 4, 8)},
+}
 HOST_FED_MAX_EDGES = 1 << 28  # the host-fed leg's sample (2 GiB of pinned host edges)
 CPU_SAMPLE_EDGES = 1 << 24    # the CPU baseline's sample (a prefix of the workload's stream)
 
@@ -794,6 +804,9 @@ def main():
                       if world > 1 else "none"),
         },
         "roofline": roofline,
+        "predicted": (dict(PREDICTED.get(args.workload, {}).get(world, {}),
+                           source="DESIGN.md §6 (per-rank folds and merge kernels measured on one GPU; all_gather modelled)")
+                      if PREDICTED.get(args.workload, {}).get(world) else None),
         "parity": parity,
         "summary": {"seen": seen, "components": comps},
         "merge": ({"ms_per_window": sum(merge_ms) / len(merge_ms), "windows_per_step": n_windows,
