@@ -354,12 +354,6 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
 #pragma unroll
         for (int k = 0; k < DEPTH; ++k) q[k] = __builtin_nontemporal_load(body + base + lane + k * stride);
     }
-    // A batch too short for the pipelined loop (C2 x 16's 2^20-edge windows: 2 rounds per wave at 256 x 1024 lanes)
-    // takes the remainder loop alone; its first round's load is issued here too, so that it lands while the bitmap is
-    // copied into LDS instead of after it (round 6; clamped in range: the compiler can count it). It goes into q[0],
-    // which the pipelined loop would have used: two or four prefetched rounds in their own registers spilled
-    bool pre = !first_round && base < n2;
-    if (pre) q[0] = __builtin_nontemporal_load(body + (base + lane < n2 ? base + lane : n2 - 1));
     const u32* bm = bits;
     if (threadIdx.x == 0) s_slow = 0;
     if constexpr (LDS) {
@@ -434,9 +428,13 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
             }
         }
     }
-    auto rest_round = [&](u32x4 q, bool valid) {
+    for (; base < n2; base += stride) {
+        const u64 i = base + lane;
+        const bool valid = i < n2;
+        u32x4 q = {0, 0, 0, 0};
+        if (valid) q = __builtin_nontemporal_load(body + i);
         u32 ea[2] = {q.x, q.z}, eb[2] = {q.y, q.w};
-        const bool v0 = valid && edge_ok(ea[0], eb[0], cap, err), v1 = valid && edge_ok(ea[1], eb[1], cap, err);
+        const bool v0 = edge_ok(ea[0], eb[0], cap, err) && valid, v1 = edge_ok(ea[1], eb[1], cap, err) && valid;
         if constexpr (HOOK) {
             const bool vv[2] = {v0, v1};
             filter_round<LDS, 2>(vv, ea, eb, bm, g, ring, wq, wd, parent, drain_at, carry2);
@@ -444,15 +442,6 @@ __global__ __launch_bounds__(BLOCK) void fold_filtered_kernel(u32* __restrict__ 
             filter_edge<LDS>(v0, ea[0], eb[0], bm, g, ring, wq, wd, parent, drain_at);
             filter_edge<LDS>(v1, ea[1], eb[1], bm, g, ring, wq, wd, parent, drain_at);
         }
-    };
-    for (; base < n2; base += stride) {
-        const u64 i = base + lane;
-        const bool valid = i < n2;
-        u32x4 qr = {0, 0, 0, 0};
-        if (pre) qr = q[0];  // the round loaded before the LDS fill
-        else if (valid) qr = __builtin_nontemporal_load(body + i);
-        pre = false;
-        rest_round(qr, valid);
     }
     if constexpr (HOOK) {  // the last rounds' hooks
         carry.settle(g, ring, wq, wd, parent, drain_at);
