@@ -621,10 +621,7 @@ def config_legs(local, steps, warmup, digests, tune, d_edges=None):
             G.generate_device(cfg, 0, E, d.data_ptr(), torch.cuda.current_stream(local).cuda_stream)
             torch.cuda.synchronize()
             starts = list(range(0, E, wedges)) + [E] if wedges else [0, E]
-            dig = digests.get(key) if key in digests else None
-            if key == "c2_rmat20/w1M":
-                dig = {"digest": digests["c2_rmat20"]["digest"], "seen": digests["c2_rmat20"]["seen"],
-                       "components": digests["c2_rmat20"]["components"]} if "c2_rmat20" in digests else None
+            dig = digests.get(key)  # every window's digest (tests/golden/make_stream_digests.py WINDOWED)
             out[key] = windows_leg(key, factory(V), wins(d.data_ptr(), starts), steps, warmup, dig, V, cfg_name,
                                    f"{cfg_name} in {len(starts) - 1} window(s), an emission per window")
             del d

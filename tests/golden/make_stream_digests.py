@@ -39,6 +39,7 @@ def entries():
 # windowed entries: name -> (config, edges per window)
 WINDOWED = {
     "c4_kron26/w8": ("c4_kron26", 1 << 27),
+    "c2_rmat20/w1M": ("c2_rmat20", 1 << 20),
     "c3_gnm24/w4M": ("c3_gnm24", 1 << 22),
     "c3_gnm24/w1M": ("c3_gnm24", 1 << 20),
     "c5_adversarial/w64K": ("c5_adversarial", 1 << 16),

@@ -189,7 +189,7 @@ def test_c4_split_8_group_merge(torch_cuda):
     torch_cuda.cuda.empty_cache()
 
 
-def emitted_windows(torch_cuda, name, knobs=None, every=1):
+def emitted_windows(torch_cuda, name, knobs=None, every=1, launches=None):
     """The LAZY emission (round 6 default, tune emit_div): per window a fold and an emission
     (gcc_forest_compress), and the summary the emission left — the forest itself, not compressed unless the amortised
     compress was due — against the oracle's digest. The check never compresses the forest under test: a second forest
@@ -202,6 +202,9 @@ def emitted_windows(torch_cuda, name, knobs=None, every=1):
     ds, chk = DisjointSet(V), DisjointSet(V)
     if knobs:
         ds.tune(**knobs)
+    if launches is not None:
+        ds.enable_timing(1)
+        ds.fold_profile()
     lazy = 0
     for w in range(len(starts) - 1):
         ds.fold_device(d.data_ptr() + 8 * starts[w], starts[w + 1] - starts[w])
@@ -214,6 +217,9 @@ def emitted_windows(torch_cuda, name, knobs=None, every=1):
         chk.reset()
         chk.merge(ds)
         check_window(chk, fx, w, f"{name} lazy")
+    if launches is not None:  # the kernels the folds and emissions launched (fold_profile names), before any read
+        launches.extend(n for n, _, _ in ds.fold_profile() if n not in ("begin", "fold_span", "slow_edges"))
+        ds.enable_timing(0)
     dig, seen, comps = ds.label_digest()  # and the labels a read materialises from it
     want = fx["windows"][-1]
     assert (str(dig), seen, comps) == (want["digest"], want["seen"], want["components"])
@@ -226,7 +232,7 @@ def emitted_windows(torch_cuda, name, knobs=None, every=1):
 
 @pytest.mark.parametrize("knobs", [None, {"emit_rec": 1}], ids=["split", "recording"])
 def test_c5_lazy_emission_every_window(torch_cuda, knobs):
-    """C5's 256 short windows at the default lazy emission (a compress per id_capacity / 8 folded edges): every
+    """C5's 256 short windows at the default lazy emission (a compress per id_capacity folded edges): every
     window's emitted summary exact, most of them uncompressed forests; with splitting folds + full compresses (default)
     and with recording folds + incremental compresses (emit_rec = 1)."""
     lazy = emitted_windows(torch_cuda, "c5_adversarial/w64K", knobs, every=4)
@@ -237,3 +243,22 @@ def test_c3_lazy_emission_every_window(torch_cuda):
     """C3 in 1M-edge windows at the default lazy emission: every window's emitted summary exact."""
     lazy = emitted_windows(torch_cuda, "c3_gnm24/w1M")
     assert lazy >= 2, lazy
+
+
+def test_c2_every_window(torch_cuda):
+    """C2 (R-MAT s20) in 16 windows of 2^20 edges at the default eager emission of the giant-filtered regime: every
+    window against the oracle (tests/golden/stream_digests.json "c2_rmat20/w1M")."""
+    fold_windows(torch_cuda, "c2_rmat20/w1M")
+
+
+def test_c2_lazy_emission_every_window(torch_cuda):
+    """C2's giant-filtered regime with the lazy emission of tune emit_filtered = 1: each emission refreshes the
+    tracked component's bitmap (the next window's filter) and writes no labels. Every window's emitted forest exact.
+    (A self-marking fold that set the bitmap bits itself, so that an emission launched nothing, measured slower:
+    profiles/r6p_ab_c2w16_self_marking_fold.txt)"""
+    launched = []
+    emitted_windows(torch_cuda, "c2_rmat20/w1M", {"emit_filtered": 1}, launches=launched)
+    # (the filtered fold hangs most ids straight under the tracked root, so "uncompressed" is not visible in the
+    # forest's depth here: the launches say what each emission did)
+    assert "compress" not in launched, launched
+    assert launched.count("refresh_bits") == 16, launched
