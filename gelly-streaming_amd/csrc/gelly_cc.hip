@@ -94,8 +94,8 @@ __device__ __forceinline__ bool edge_ok(u32& a, u32& b, u32 cap, u32* err) {
     return ok;
 }
 
-// Kernel-start trace (diagnostics, always on): block 0's thread 0 of each traced kernel stores the kernel's id into
-// one pinned host word (system scope, a vector store). A stream's kernels start in order and a fault stops its
+// Kernel-start trace (diagnostics, GELLY_TRACE=1): block 0's thread 0 of each traced kernel stores the kernel's id
+// into one pinned host word (system scope, a vector store). A stream's kernels start in order and a fault stops its
 // queue, so after an asynchronous fault the word names the kernel that faulted (or one of another stream).
 __device__ u32* gcc_trace_slot = nullptr;
 enum : u32 {
@@ -3761,6 +3761,10 @@ extern "C++" const char* gcc_fault_note(hipError_t e) {  // abi_common.h (C++ li
 
 static int set_trace_slot() {  // the current device
     std::call_once(g_trace_once, [] {
+        // opt-in (GELLY_TRACE=1): the system-scope store costs the shortest launches (C2 x 16: 0.259 vs 0.267 ms per
+        // step, profiles/r6u_ab_kernel_start_trace.txt)
+        const char* e = std::getenv("GELLY_TRACE");
+        if (!e || !*e || e[0] == '0') return;
         if (hipHostMalloc((void**)&g_trace_host, 64, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
             g_trace_host = nullptr;
         else
