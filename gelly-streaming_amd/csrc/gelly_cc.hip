@@ -2091,6 +2091,10 @@ struct FoldTune {
     double refresh[3] = {0.04, 0.12, 0.30};
     bool filter = true;
     double filter_min_share = 0.5;  // the voted component must hold this share of the seen samples (0: no check)
+    // the share is read back asynchronously (1): the sampled start does not wait for the device; the batch's rest
+    // folds plain (correct either way) and the first fold that finds the share landed turns the filter on if it
+    // holds. 0: the host waits for the vote mid-batch (rounds 1-5)
+    int share_async = 1;
     int depth = 4;  // 16-B edge-pair loads in flight per lane in the filtered kernel (4 or 8)
     // seeded fold of a fresh forest (seed_* kernels): BFS from a hub over the first 1/seed_div of the batch
     bool seed = true;
@@ -2236,6 +2240,11 @@ struct gcc_forest {
     // first window, e.g. C5's 2^15-edge chunks at N = 2, went straight to the filtered regime over a component of a few
     // ids, and the filtered fold keeps no delta lists). launch_fold reads the share once and decides filter_off
     bool share_unchecked = false;
+    // the sampled start's vote-share check read back without a host sync (FoldTune::share_async): the share lands in
+    // h_share behind share_ev, the batch's rest and later batches fold plain until a fold finds the event complete
+    bool share_pending = false;
+    hipEvent_t share_ev = nullptr;
+    u32* h_share = nullptr;
     int giant_slot = 0;  // d_giant[giant_slot] = root of the tracked component as of the last refresh
     u32* d_qcount = nullptr;  // per-block slow-edge counts of the last filtered launch (measurement)
     // fused seeding: dedicated flag bytes (one per id, rounded up to a bitmap word), marked with an epoch
@@ -3317,6 +3326,20 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     return GCC_OK;
 }
 
+// The sampled start's share, read back without a host sync (FoldTune::share_async): not landed yet -> nothing (this
+// batch folds plain, as every batch since the vote did); landed -> the filter turns on if the voted component holds
+// filter_min_share of the samples, after a refresh of its bitmap (the empty set until then).
+static int share_poll(gcc_forest* h) {
+    const hipError_t q = hipEventQuery(h->share_ev);
+    if (q == hipErrorNotReady) return GCC_OK;
+    HIP_TRY(q);
+    h->share_pending = false;
+    const u32 hit = __atomic_load_n(&h->h_share[0], __ATOMIC_ACQUIRE), seen = __atomic_load_n(&h->h_share[1], __ATOMIC_ACQUIRE);
+    if (!h->has_giant || hit < h->tune.filter_min_share * seen) return GCC_OK;
+    h->filter_off = false;
+    return refresh_now(h);
+}
+
 // The fold pipeline for one batch (UpdateCC.foldEdges over the batch, DisjointSet.union per edge):
 //  0. a FRESH forest (reset, nothing folded since) is seeded: launch_seed builds the component of a hub
 //     over a prefix on a bitmap and writes parent[] from it; the filtered kernel then folds the whole batch;
@@ -3359,6 +3382,7 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
         }
         return GCC_OK;
     }
+    if (h->share_pending && !h->pending_reset && (rc = share_poll(h))) return rc;
     if (h->share_unchecked && !h->pending_reset) {
         h->share_unchecked = false;
         if (h->has_giant && !h->filter_off && h->filter_enabled() && t.filter_min_share > 0 && h->d_giant) {
@@ -3399,10 +3423,20 @@ static int launch_fold(gcc_forest* h, const u32* d_pairs, u64 n) {
                               h->d_giant + h->giant_slot, h->d_giant + 4);
             if (rc) return rc;
             h->has_giant = true;
-            u32 share[2] = {0, 0};
-            HIP_TRY(hipMemcpyAsync(share, h->d_giant + 4, sizeof(share), hipMemcpyDeviceToHost, h->stream));
-            HIP_TRY(hipStreamSynchronize(h->stream));
-            h->filter_off = share[0] < t.filter_min_share * share[1];
+            if (t.share_async) {
+                // the batch's rest folds plain while the share travels; a later fold decides (share_poll)
+                if (!h->h_share) HIP_TRY(hipHostMalloc((void**)&h->h_share, 2 * sizeof(u32), hipHostMallocDefault));
+                if (!h->share_ev) HIP_TRY(hipEventCreateWithFlags(&h->share_ev, hipEventDisableTiming));
+                HIP_TRY(hipMemcpyAsync(h->h_share, h->d_giant + 4, 2 * sizeof(u32), hipMemcpyDeviceToHost, h->stream));
+                HIP_TRY(hipEventRecord(h->share_ev, h->stream));
+                h->share_pending = true;
+                h->filter_off = true;
+            } else {
+                u32 share[2] = {0, 0};
+                HIP_TRY(hipMemcpyAsync(share, h->d_giant + 4, sizeof(share), hipMemcpyDeviceToHost, h->stream));
+                HIP_TRY(hipStreamSynchronize(h->stream));
+                h->filter_off = share[0] < t.filter_min_share * share[1];
+            }
             if (!h->filter_off) rc = refresh_now(h);
             else  // no refresh: the tracked-component bitmap is the empty set (valid: components only grow)
                 HIP_TRY(hipMemsetAsync(h->d_bits, 0, (size_t)h->nwords() * sizeof(u64), h->stream));
@@ -3895,6 +3929,8 @@ int gcc_forest_destroy(gcc_forest* h) {
         (void)hipStreamDestroy(h->pipe_stream);
     }
     if (h->pipe_ev_fold) (void)hipEventDestroy(h->pipe_ev_fold);
+    if (h->share_ev) (void)hipEventDestroy(h->share_ev);
+    if (h->h_share) (void)hipHostFree(h->h_share);
     if (h->aux_stream) {
         (void)hipStreamSynchronize(h->aux_stream);
         (void)hipStreamDestroy(h->aux_stream);
@@ -4032,6 +4068,7 @@ int gcc_forest_reset(gcc_forest* h) {
     h->has_giant = false;  // the giant bitmap described the old forest
     h->filter_off = false;
     h->share_unchecked = false;
+    h->share_pending = false;
     h->edges_since_compress = 0;
     h->delta_armed = false;
     return GCC_OK;
@@ -4671,6 +4708,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "seed_div1") t.seed_div1 = std::max<u64>(1, (u64)value);
     else if (k == "seed_refresh") t.seed_refresh = value;
     else if (k == "seed_fuse") t.seed_fuse = value != 0;
+    else if (k == "share_async") t.share_async = value != 0;
     else if (k == "filter_min_share") t.filter_min_share = value;
     else if (k == "incremental") t.incremental = value != 0;
     else if (k == "inc_inplace") t.inc_inplace = value != 0;

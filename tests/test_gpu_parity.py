@@ -535,7 +535,7 @@ KNOB_CASES = {
     "sample_growth": {"sample_growth": 2}, "sample_div": {"sample_div": 8}, "sample_min": {"sample_min": 4096},
     "refresh_min_batch": {"refresh_min_batch": 1024}, "refresh1": {"refresh_min_batch": 1024, "refresh1": 0.1},
     "refresh2": {"refresh_min_batch": 1024, "refresh2": 0.2}, "refresh3": {"refresh_min_batch": 1024, "refresh3": 0.6},
-    "depth": {"depth": 8}, "hook": {"hook": 0}, "drain_at": {"drain_at": 1}, "seed": {"seed": 0},
+    "depth": {"depth": 8}, "hook": {"hook": 0}, "share_async": {"share_async": 0}, "drain_at": {"drain_at": 1}, "seed": {"seed": 0},
     "seed_nt": {"seed_nt": 0}, "seed_global": {"seed_global": 1}, "seed_fuse": {"seed_fuse": 0},
     "seed_passes": {"seed_passes": 3}, "seed_div": {"seed_div": 2}, "seed_div1": {"seed_div1": 5},
     "seed_refresh": {"seed_refresh": 0.5}, "incremental": {"inc_min_ids": 1024, "incremental": 1},
