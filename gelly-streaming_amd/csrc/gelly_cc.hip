@@ -2081,7 +2081,9 @@ static inline unsigned grid_for(u64 n, unsigned max_blocks) {
 // fold pipeline tuning (defaults measured on C2, tools/sweep_fold.py; gcc_forest_tune overrides)
 struct FoldTune {
     u64 filter_min_batch = 1ull << 16;  // below this a fresh forest's batch is folded by fold_kernel alone
-    u64 sample_first = 1ull << 12;      // first sampling launch; each next one is sample_growth x larger
+    // first sampling launch; each next one is sample_growth x larger (round 6: 2^14, one launch fewer than 2^12: C3
+    // 1.040 -> 1.028 ms, C5 and C3 in 1M-edge windows unchanged within noise, profiles/r6z_sweep_sampled_start.txt)
+    u64 sample_first = 1ull << 14;
     u64 sample_growth = 4;
     u64 sample_div = 128;               // the sampling prefix is 1/sample_div of a fresh forest's first batch
     u64 sample_min = 9ull << 15;        // ... and at least this many edges (C3: a shorter prefix left more CAS work)
