@@ -262,3 +262,15 @@ def test_c2_lazy_emission_every_window(torch_cuda):
     # forest's depth here: the launches say what each emission did)
     assert "compress" not in launched, launched
     assert launched.count("refresh_bits") == 16, launched
+
+
+def test_c2_sampled_start_turns_the_filter_on_later(torch_cuda):
+    """The vote-share check without a host sync (tune share_async, round 6): a fresh forest that is not seeded (seed =
+    0) votes in its first window and folds that window's rest plain while the share travels; a later window finds the
+    share landed, refreshes the bitmap and takes the giant-filtered fold. Every window's summary exact, and the
+    filtered kernel did run."""
+    launched = []
+    emitted_windows(torch_cuda, "c2_rmat20/w1M", {"seed": 0}, launches=launched)
+    assert "vote" in launched and "plain" in launched, launched
+    first_filtered = launched.index("filtered") if "filtered" in launched else -1
+    assert first_filtered > launched.index("vote"), launched
