@@ -2175,6 +2175,9 @@ struct FoldTune {
     int bucket_p2_per = 12;
     int bucket_p2_vw = 4;      // FINAL P2's write-out: v-list entries per lane (4: 8-B + 4-B stores; 8: 16-B + 8-B)
     int bucket_chunk = 0;      // entries per chunk reservation in the bucketed fold's lists (0: by batch size)
+    // diagnostics (tools/placement_probe.py): the next bucketed fold takes freshly allocated scratch (1: every list;
+    // 2: the bucket storage only; 3: the v-lists only), the old buffers held a while so the new ones land elsewhere
+    int scratch_realloc = 0;
     // the bucketed fold also for a later window of a forest tracking a giant (C4 in 8 windows: every window after the
     // first took the filtered fold over an 8 MiB global bitmap, 2.2 ms per 2^27 edges; round 4)
     int bucket_windows = 1;
@@ -2318,6 +2321,7 @@ struct gcc_forest {
 
     // bucketed fold (bucket_fold.h): metadata, bucket storage, overflow list, v-lists (grown on demand)
     bk::Meta* d_meta = nullptr;
+    std::vector<void*> held_scratch;  // FoldTune::scratch_realloc: earlier scratch buffers, freed two generations on
     uint8_t* d_bk = nullptr;  // bucket storage: bk::bk_bytes(S) bytes = S 6-B entries (lo array, then hi array)
     u64 bk_cap_bytes = 0;
     u64* d_ovf = nullptr;
@@ -3068,6 +3072,33 @@ static int launch_bucket(gcc_forest* h, const u32* d_pairs, u64 n) {
     const u32 p1_blocks = 2 * (u32)h->n_cu;  // (bucket_p1 = 1 runs n_cu blocks: fewer writers, same slack bound)
     const u32 p2_blocks = std::min<u32>((u32)h->n_cu, bk::kMaxP2Blocks);
     const u32 chunk = bk::chunk_entries(n, (u32)t.bucket_chunk);
+    if (h->tune.scratch_realloc) {  // diagnostics: fresh scratch for this fold
+        const int mode = h->tune.scratch_realloc;
+        h->tune.scratch_realloc = 0;
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        while (h->held_scratch.size() > 8) {
+            (void)hipFree(h->held_scratch.front());
+            h->held_scratch.erase(h->held_scratch.begin());
+        }
+        if ((mode == 1 || mode == 2) && h->d_bk) {
+            h->held_scratch.push_back(h->d_bk);
+            h->d_bk = nullptr;
+            h->bk_cap_bytes = 0;
+        }
+        if ((mode == 1 || mode == 3) && h->d_vl) {
+            h->held_scratch.push_back(h->d_vl);
+            h->d_vl = nullptr;
+            h->vl_cap = 0;
+        }
+        if (mode == 1) {
+            if (h->d_slow) h->held_scratch.push_back(h->d_slow);
+            if (h->d_ovf) h->held_scratch.push_back(h->d_ovf);
+            h->d_slow = nullptr;
+            h->slow_cap_total = 0;
+            h->d_ovf = nullptr;
+            h->ovf_cap = 0;
+        }
+    }
     const u64 bk_S = bk::bk_entries(bk::storage_edges(n, ns, p1_blocks, bk::bk_aligned(n), chunk));  // entries (a multiple of 2^19)
     if ((rc = grow(h->d_bk, h->bk_cap_bytes, bk::bk_bytes(bk_S), h->stream))) return rc;
     u32* bk_lo = reinterpret_cast<u32*>(h->d_bk);
@@ -3973,6 +4004,7 @@ int gcc_forest_destroy(gcc_forest* h) {
     if (h->d_counts) (void)hipFree(h->d_counts);
     if (h->d_err) (void)hipFree(h->d_err);
     if (h->d_meta) (void)hipFree(h->d_meta);
+    for (void* p : h->held_scratch) (void)hipFree(p);
     if (h->d_bk) (void)hipFree(h->d_bk);
     if (h->d_ovf) (void)hipFree(h->d_ovf);
     if (h->d_vl) (void)hipFree(h->d_vl);
@@ -4737,6 +4769,7 @@ int gcc_forest_tune(gcc_forest* h, const char* key, double value) {
     else if (k == "bucket_p1") t.bucket_p1 = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_p2_per") t.bucket_p2_per = (int)value == 12 ? 12 : 8;
     else if (k == "bucket_p2_vw") t.bucket_p2_vw = (int)value == 8 ? 8 : 4;
+    else if (k == "scratch_realloc") t.scratch_realloc = std::max(0, std::min(3, (int)value));
     else if (k == "bucket_chunk") t.bucket_chunk = std::max(0, std::min((int)bk::kMaxChunk, (int)value));
     else if (k == "bucket_windows") t.bucket_windows = value != 0;
     else if (k == "bucket_items") t.bucket_items = std::max(1, std::min(64, (int)value));

@@ -550,6 +550,7 @@ KNOB_CASES = {
     "bucket_sample": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_sample": 1.0},
     "bucket_sample_sparse": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_sample_sparse": 0.05},
     "pin_chunk": {"pin_chunk": 4096},
+    "scratch_realloc": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "scratch_realloc": 1},
     "bucket_p1": [{"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 0},
                   {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_p1": 3}],
     "bucket_slow2": {"bucket_min_ids": 0, "bucket_min_batch": 1 << 16, "bucket_slow2": 0},
