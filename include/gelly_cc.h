@@ -347,7 +347,7 @@ int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, 
  * drain_at, seed, seed_nt, seed_global, seed_fuse, seed_passes, seed_div, seed_div1, seed_refresh, incremental,
  * inc_min_ids, inc_div, inc_inplace, inc_check, post_check, inc_split, fold_release, experimental, refresh_labels, bucket,
  * bucket_min_batch, bucket_min_ids, bucket_levels, bucket_sample, bucket_sample_sparse, bucket_hub_sample, bucket_p1, bucket_p2_per, bucket_p2_vw,
- * bucket_chunk, bucket_windows, bucket_items, bucket_items_p3,
+ * bucket_chunk, scratch_realloc, bucket_windows, bucket_items, bucket_items_p3,
  * bucket_slow2, bucket_defer, bucket_defer_c, compress_split, fold_split, inc_pipe, emit_div, emit_rec, emit_filtered,
  * pin_chunk, lds_edges_per_word. Unknown keys return GCC_E_INVALID.
  * emit_div (round 6): the lazy emission — in the plain regime (no tracked giant) gcc_forest_compress compresses only
