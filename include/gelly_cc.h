@@ -355,7 +355,10 @@ int gcc_idmap_canonical(gcc_idmap* m, const uint32_t* dense_labels, uint64_t n, 
  * the forest it leaves is the emitted summary (exact for find: every root is its component's minimum id), and every
  * read (labels, find, size, digest, serialize, a merge message) compresses first. emit_rec: the folds between lazy
  * emissions record for an incremental compress (1) or split paths (0). emit_filtered: in the giant-filtered regime the
- * emission refreshes only the tracked component's bitmap (1) or compresses (0). One more key is a test hook, not a speed knob: fail_absorb = n makes the n-th next absorb fail with
+ * emission refreshes only the tracked component's bitmap (1) or compresses (0). share_async (round 6, default 1): a fresh forest's
+ * vote-share check is read back behind an event instead of a host sync, the batch's rest folds plain meanwhile, and a
+ * later fold turns the giant filter on once the share has landed (0: wait for it mid-batch). scratch_realloc
+ * (diagnostics, tools/placement_probe.py): the next bucketed fold takes freshly allocated scratch lists. One more key is a test hook, not a speed knob: fail_absorb = n makes the n-th next absorb fail with
  * GCC_E_INTERNAL before it launches anything (a rank's failure inside the cross-GPU group merge).
  * One setting is known to give wrong results and is refused (GCC_E_INVALID) unless `experimental` is set to 1 first:
  * inc_split = 1 (path splitting in the recording fold before an in-place incremental compress: round 3's stale label,
